@@ -1,0 +1,526 @@
+// LLM.int8 hot path on gfx950: row/col statistics, double_quant, tile layouts,
+// igemmlt on the int8 MFMA and the int32 -> fp16 dequant (standalone and fused).
+//
+// Replaces (same C-ABI names, argument order and meaning):
+//   cget_col_row_stats            ref:sycl/pythonInterface.cpp:335  -> kgetColRowStats    kernel_quant.cpp:3214-3379
+//   cdouble_rowcol_quant          ref:sycl/pythonInterface.cpp:338  -> kDoubleRowColQuant kernel_quant.cpp:3384-3512
+//   ctransform_row2{col32,turing,ampere}{,T}  ref:sycl/pythonInterface.cpp:341-357 -> kTransformRowToFormat 3516-3840
+//   cigemmlt_{turing,ampere}_{32,8,8_rowscale} ref:sycl/pythonInterface.cpp:298-316 -> igemmlt op_gemm.cpp:541-655
+//   cdequant_mm_int32_fp16        ref:sycl/pythonInterface.cpp:333  -> kdequant_mm_int32_fp16 kernel_quant.cpp:3846-3987
+//   cextractOutliers_{turing,ampere} ref:sycl/pythonInterface.cpp:368-369 -> kExtractOutliers 3992-
+// Additive: ctransform_{turing,ampere,col32}2row (called by functional.py:2645-2647, never exported by the
+// reference, Q18) and cigemmlt_row_dequant_fp16 (row-major int8 A and B, int32 accumulators dequantised
+// to fp16 in the epilogue = igemmlt + mm_dequant in one launch).
+//
+// Layout maps (offset of element (r, c) of a [rows, cols] matrix), blas_utils.h:244-346:
+//   col32      (c/32)*ld + 32 r + c%32                                  ld = 32*rows
+//   col_turing (c/32)*ld + (r/8)*256 + 128(r%2) + 16((c%32)/4) + 4((r%8)/2) + c%4     ld = 32*pad8(rows)
+//   col_ampere (c/32)*ld + (r/32)*1024 + 32*arow(r%32) + c%32, arow(x) = 8((x%8)/2) + 2(x/8) + x%2   ld = 32*pad32(rows)
+#include "common.hpp"
+
+namespace bnb {
+
+enum Fmt { ROW = 0, COL32 = 2, TURING = 3, AMPERE = 4 };
+
+__host__ __device__ __forceinline__ long long pad_to(long long v, long long m) { return (v + m - 1) / m * m; }
+
+__device__ __forceinline__ int ampere_row(int x) { return 8 * ((x & 7) >> 1) + 2 * (x >> 3) + (x & 1); }
+
+// offset of element (r, c) in format F, `ld` = the format's leading dimension (see header)
+template <int F>
+__device__ __forceinline__ long long fmt_offset(long long r, long long c, long long ld) {
+  if constexpr (F == ROW) return r * ld + c;
+  else if constexpr (F == COL32) return (c >> 5) * ld + 32 * r + (c & 31);
+  else if constexpr (F == TURING)
+    return (c >> 5) * ld + (r >> 3) * 256 + 128 * (r & 1) + 16 * ((c & 31) >> 2) + 4 * ((r & 7) >> 1) + (c & 3);
+  else return (c >> 5) * ld + (r >> 5) * 1024 + 32 * ampere_row((int)(r & 31)) + (c & 31);
+}
+
+// ============================================================================ row/col statistics
+// Tile: 16 rows x 256 cols per 256-thread workgroup (the reference's TILE_ROWS/TILE_COLS, which also
+// fix the layout of nnz_count_row: entry (tile*16 + r + 1), tile = row_tile*col_tiles + col_tile).
+// Thread t: 8 consecutive columns (t%32) of rows (t/32) and (t/32)+8.
+
+__device__ __forceinline__ void load8_half(const fp16_t* A, long long row, int c0, int cols, bool vec, float (&v)[8]) {
+  const fp16_t* p = A + row * (long long)cols + c0;
+  if (vec && c0 + 8 <= cols) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[i] & 0xFFFF));
+      v[2 * i + 1] = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[i] >> 16));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (c0 + i < cols) ? (float)p[i] : 0.0f;
+  }
+}
+
+__device__ __forceinline__ void atomic_max_nonneg(float* addr, float v) {
+  // valid for v >= 0 against any existing value (negative init or non-negative maxima)
+  atomicMax(reinterpret_cast<int*>(addr), __float_as_int(v));
+}
+
+template <bool SPARSE>
+__global__ void __launch_bounds__(256)
+k_colrow_stats(const fp16_t* __restrict__ A, float* __restrict__ rowStats, float* __restrict__ colStats,
+               int* __restrict__ nnz_count_row, float threshold, int rows, int cols, int col_tiles, bool vec) {
+  __shared__ float s_col[8][256];
+  __shared__ int s_nnz[16];
+  const int tid = threadIdx.x;
+  const int row_tile = blockIdx.x / col_tiles, col_tile = blockIdx.x % col_tiles;
+  const int base_row = row_tile * 16, base_col = col_tile * 256;
+  const int cg = tid & 31, rs = tid >> 5;
+  const int c0 = base_col + 8 * cg;
+  if (tid < 16) s_nnz[tid] = 0;
+  float cmax[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cmax[i] = -3.402823466e+38f;
+  float rmax[2];
+  int rnnz[2] = {0, 0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = base_row + rs + 8 * h;
+    rmax[h] = -3.402823466e+38f;
+    if (row < rows && c0 < cols) {
+      float v[8];
+      load8_half(A, row, c0, cols, vec, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float a = fabsf(v[i]);
+        if (c0 + i >= cols) a = -3.402823466e+38f;
+        if (SPARSE && c0 + i < cols && a >= threshold) { rnnz[h] += 1; a = 0.0f; }
+        cmax[i] = fmaxf(cmax[i], a);
+        rmax[h] = fmaxf(rmax[h], a);
+      }
+    }
+    // row reduce over the 32 lanes that share this row (lanes 0-31 / 32-63 of the wave)
+    rmax[h] = wave_max_xor(rmax[h], 32);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = base_row + rs + 8 * h;
+    if ((tid & 31) == 0 && row < rows && rmax[h] >= 0.0f) atomic_max_nonneg(&rowStats[row], rmax[h]);
+    if (SPARSE) {
+      int c = rnnz[h];
+      for (int o = 1; o < 32; o <<= 1) c += __shfl_xor(c, o, 64);
+      if ((tid & 31) == 0) s_nnz[rs + 8 * h] = c;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s_col[rs][8 * cg + i] = cmax[i];
+  __syncthreads();
+  {
+    float m = s_col[0][tid];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) m = fmaxf(m, s_col[r][tid]);
+    const int col = base_col + tid;
+    if (col < cols && m >= 0.0f) atomic_max_nonneg(&colStats[col], m);
+  }
+  if (SPARSE && tid < 16) nnz_count_row[blockIdx.x * 16 + tid + 1] = s_nnz[tid];
+}
+
+// ============================================================================ double row/col quant
+
+__device__ __forceinline__ int8_t rint_i8(float v) {
+  // (char)rint(v): half-to-even; NaN -> 0; saturating (|v| <= 127 for in-range data)
+  float r = rintf(v);
+  if (r != r) r = 0.0f;
+  r = fminf(fmaxf(r, -128.0f), 127.0f);
+  return (int8_t)(int)r;
+}
+
+template <bool SPARSE>
+__global__ void __launch_bounds__(256)
+k_double_rowcol_quant(const fp16_t* __restrict__ A, const float* __restrict__ rowStats,
+                      const float* __restrict__ colStats, int8_t* __restrict__ out_col, int8_t* __restrict__ out_row,
+                      int* __restrict__ rowidx, int* __restrict__ colidx, fp16_t* __restrict__ val,
+                      const int* __restrict__ nnz_block_ptr, float threshold, int rows, int cols, int col_tiles,
+                      bool vec) {
+  __shared__ unsigned s_next[16];
+  const int tid = threadIdx.x;
+  const int row_tile = blockIdx.x / col_tiles, col_tile = blockIdx.x % col_tiles;
+  const int base_row = row_tile * 16, base_col = col_tile * 256;
+  const int cg = tid & 31, rs = tid >> 5;
+  const int c0 = base_col + 8 * cg;
+  if (SPARSE) {
+    if (tid < 16) s_next[tid] = (unsigned)nnz_block_ptr[blockIdx.x * 16 + tid];
+    __syncthreads();
+  }
+  if (c0 >= cols) return;
+  float cs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cs[i] = (c0 + i < cols) ? __fdiv_rn(127.0f, colStats[c0 + i]) : 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = base_row + rs + 8 * h;
+    if (row >= rows) continue;
+    float v[8];
+    load8_half(A, row, c0, cols, vec, v);
+    const float rsc = __fdiv_rn(127.0f, rowStats[row]);
+    uint32_t qr[2] = {0, 0}, qc[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int8_t r8 = rint_i8(__fmul_rn(v[i], rsc));
+      if (SPARSE && c0 + i < cols && fabsf(v[i]) >= threshold) {
+        r8 = 0;
+        const unsigned slot = atomicAdd(&s_next[rs + 8 * h], 1u);
+        rowidx[slot] = row;
+        colidx[slot] = c0 + i;
+        val[slot] = (fp16_t)v[i];
+      }
+      const int8_t c8 = rint_i8(__fmul_rn(v[i], cs[i]));
+      qr[i >> 2] |= (uint32_t)(uint8_t)r8 << (8 * (i & 3));
+      qc[i >> 2] |= (uint32_t)(uint8_t)c8 << (8 * (i & 3));
+    }
+    const long long off = (long long)row * cols + c0;
+    if (vec && c0 + 8 <= cols) {
+      *reinterpret_cast<uint2*>(out_row + off) = make_uint2(qr[0], qr[1]);
+      *reinterpret_cast<uint2*>(out_col + off) = make_uint2(qc[0], qc[1]);
+    } else {
+      for (int i = 0; i < 8 && c0 + i < cols; ++i) {
+        out_row[off + i] = (int8_t)(qr[i >> 2] >> (8 * (i & 3)));
+        out_col[off + i] = (int8_t)(qc[i >> 2] >> (8 * (i & 3)));
+      }
+    }
+  }
+}
+
+// ============================================================================ layout transforms
+// One thread per element (row-major source index i).  These are load-time / small-tensor ops.
+
+template <int F, bool TRANSPOSE, bool INVERSE>
+__global__ void k_transform(const int8_t* __restrict__ src, int8_t* __restrict__ dst, int rows, int cols) {
+  const long long n = (long long)rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cols, c = i % cols;
+    // logical matrix in the target format: A (rows x cols) or A^T (cols x rows)
+    const long long lr = TRANSPOSE ? c : r, lc = TRANSPOSE ? r : c;
+    const long long lrows = TRANSPOSE ? cols : rows;
+    long long ld;
+    if constexpr (F == COL32) ld = 32 * lrows;
+    else if constexpr (F == TURING) ld = 32 * pad_to(lrows, 8);
+    else ld = 32 * pad_to(lrows, 32);
+    const long long o = fmt_offset<F>(lr, lc, ld);
+    if (INVERSE) dst[i] = src[o];
+    else dst[o] = src[i];
+  }
+}
+
+template <int F, bool TRANSPOSE, bool INVERSE>
+static void launch_transform(const int8_t* A, int8_t* out, int rows, int cols) {
+  const long long n = (long long)rows * cols;
+  if (n <= 0) return;
+  long long g = (n + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL((k_transform<F, TRANSPOSE, INVERSE>), dim3((unsigned)g), dim3(256), 0, current_stream(), A, out, rows, cols);
+  BNB_LAUNCH_CHECK("transform");
+}
+
+// ============================================================================ dequant_mm_int32_fp16
+
+// out[r, c] = half( ((float(C[r,c]) * 6.200012e-05f) * rowStats[r]) * colStats[c] + bias[c] )
+// (kernel_quant.cpp:3969 operation order; explicit _rn ops forbid FMA contraction)
+__device__ __forceinline__ fp16_t mm_dequant_value(int32_t acc, float rs, float cs, float bias) {
+  float v = __fmul_rn((float)acc, 6.200012e-05f);
+  v = __fmul_rn(v, rs);
+  v = opaque(__fmul_rn(v, cs));   // keep mul and add separately rounded (no v_fma_mix fold)
+  v = __fadd_rn(v, bias);
+  return Io<fp16_t>::from_f32(v);
+}
+
+// C in col32 layout (the reference's igemmlt output, ldc = 32*numRows); 4 consecutive columns per thread
+__global__ void __launch_bounds__(256)
+k_dequant_mm_col32(const int32_t* __restrict__ C, const float* __restrict__ rowStats, const float* __restrict__ colStats,
+                   fp16_t* __restrict__ out, const fp16_t* __restrict__ bias, int numRows, int numCols) {
+  const long long groups = (long long)numRows * ((numCols + 3) / 4);
+  const int cgroups = (numCols + 3) / 4;
+  for (long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(g / cgroups), c0 = 4 * (int)(g % cgroups);
+    const float rs = rowStats[r];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + j;
+      if (c >= numCols) break;
+      const int32_t acc = C[(long long)(c >> 5) * 32 * numRows + 32LL * r + (c & 31)];
+      out[(long long)r * numCols + c] = mm_dequant_value(acc, rs, colStats[c], bias ? (float)bias[c] : 0.0f);
+    }
+  }
+}
+
+// ============================================================================ igemmlt (int8 MFMA)
+// C[i, j] = sum_k A[i, k] * B[j, k]   (A m x k, B n x k, both K-contiguous per row)
+// 128 x 128 output tile per 256-thread workgroup (2x2 waves, 64x64 per wave, v_mfma_i32_16x16x64_i8),
+// BK = 128 bytes, two LDS stages with register staging (issue loads before the MFMA phase, write to
+// LDS after the next barrier).  Operand fragments: lane l holds 16 consecutive k of row (l&15),
+// k-chunk (l>>4) — the same k assignment for A and B, so the dot product is exact for any internal
+// k order of the instruction.
+
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+
+enum Epi { EPI_I32_COL32 = 0, EPI_I8_COL32 = 1, EPI_I8_COL32_ROWSCALE = 2, EPI_F16_ROW_DEQUANT = 3, EPI_I32_ROW = 4 };
+
+constexpr int Q_BM = 128, Q_BN = 128, Q_BK = 128, Q_THREADS = 256;
+constexpr int Q_TILE = Q_BM * Q_BK;   // 16 KiB
+
+__device__ __forceinline__ int qswz(int r, int s) { return r * 128 + ((s ^ (r & 7)) << 4); }
+
+// Stage one 128 x 128 operand tile into registers: thread t -> row t>>1, k-half (t&1)*64, 4 x 16 B.
+template <int F>
+__device__ __forceinline__ void load_tile(const int8_t* __restrict__ P, long long ld, int row0, int nrows, int k0,
+                                          int K, uint4 (&v)[4]) {
+  const int tr = threadIdx.x >> 1, th = threadIdx.x & 1;
+  const long long r = min(row0 + tr, nrows - 1);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = k0 + 64 * th + 16 * s;
+    if (k + 16 <= K) {
+      if constexpr (F == TURING) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = *reinterpret_cast<const uint32_t*>(P + fmt_offset<F>(r, k + 4 * q, ld));
+        v[s] = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        v[s] = *reinterpret_cast<const uint4*>(P + fmt_offset<F>(r, k, ld));
+      }
+    } else {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int b = 0; b < 16; ++b)
+        if (k + b < K) w[b >> 2] |= (uint32_t)(uint8_t)P[fmt_offset<F>(r, k + b, ld)] << (8 * (b & 3));
+      v[s] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+__device__ __forceinline__ void store_tile(uint8_t* lds, const uint4 (&v)[4]) {
+  const int tr = threadIdx.x >> 1, th = threadIdx.x & 1;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) *reinterpret_cast<uint4*>(lds + qswz(tr, 4 * th + s)) = v[s];
+}
+
+template <int AF, int BF, int EPI>
+__global__ void __launch_bounds__(Q_THREADS, 2)
+k_igemm(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restrict__ B, void* __restrict__ Cout,
+        const float* __restrict__ row_scale, long long lda, long long ldb, long long ldc,
+        const float* __restrict__ rowStats, const float* __restrict__ colStats, const fp16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * Q_TILE];
+  uint8_t* As = smem;
+  uint8_t* Bs = smem + 2 * Q_TILE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  const int tilesN = (N + Q_BN - 1) / Q_BN, tilesM = (M + Q_BM - 1) / Q_BM;
+  const int nwg = tilesN * tilesM;
+  int wg = blockIdx.x;
+  {
+    const int xcd = wg & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (wg >> 3);
+  }
+  constexpr int GROUP = 8;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * Q_BM, n0 = tn * Q_BN;
+
+  const int wm = wave >> 1, wn = wave & 1;
+  i32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = i32x4_t{0, 0, 0, 0};
+
+  const int nk = (K + Q_BK - 1) / Q_BK;
+  uint4 ra[4], rb[4];
+  load_tile<AF>(A, lda, m0, M, 0, K, ra);
+  load_tile<BF>(B, ldb, n0, N, 0, K, rb);
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    uint8_t* as = As + cur * Q_TILE;
+    uint8_t* bs = Bs + cur * Q_TILE;
+    store_tile(as, ra);
+    store_tile(bs, rb);
+    __syncthreads();
+    if (t + 1 < nk) {
+      load_tile<AF>(A, lda, m0, M, (t + 1) * Q_BK, K, ra);
+      load_tile<BF>(B, ldb, n0, N, (t + 1) * Q_BK, K, rb);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 a[4], b[4];
+      const int slot = 4 * ks + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const uint4*>(as + qswz(64 * wm + 16 * i + (lane & 15), slot));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + qswz(64 * wn + 16 * j + (lane & 15), slot));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a[i]),
+                                                            __builtin_bit_cast(i32x4_t, b[j]), acc[i][j], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + 64 * wm + 16 * i + 4 * (lane >> 4) + r;
+      if (row >= M) continue;
+      float rs = 0.0f;
+      if constexpr (EPI == EPI_F16_ROW_DEQUANT) rs = rowStats[row];
+      if constexpr (EPI == EPI_I8_COL32_ROWSCALE) rs = row_scale[row];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + 64 * wn + 16 * j + (lane & 15);
+        if (col >= N) continue;
+        const int32_t v = acc[i][j][r];
+        if constexpr (EPI == EPI_I32_COL32) {
+          reinterpret_cast<int32_t*>(Cout)[fmt_offset<COL32>(row, col, ldc)] = v;
+        } else if constexpr (EPI == EPI_I32_ROW) {
+          reinterpret_cast<int32_t*>(Cout)[(long long)row * ldc + col] = v;
+        } else if constexpr (EPI == EPI_I8_COL32) {
+          reinterpret_cast<int8_t*>(Cout)[fmt_offset<COL32>(row, col, ldc)] = rint_i8((float)v);
+        } else if constexpr (EPI == EPI_I8_COL32_ROWSCALE) {
+          reinterpret_cast<int8_t*>(Cout)[fmt_offset<COL32>(row, col, ldc)] = rint_i8(__fmul_rn((float)v, rs));
+        } else {
+          reinterpret_cast<fp16_t*>(Cout)[(long long)row * ldc + col] =
+              mm_dequant_value(v, rs, colStats[col], bias ? (float)bias[col] : 0.0f);
+        }
+      }
+    }
+  }
+}
+
+template <int AF, int BF, int EPI>
+static int launch_igemm(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale, long long lda,
+                        long long ldb, long long ldc, const float* rowStats = nullptr, const float* colStats = nullptr,
+                        const fp16_t* bias = nullptr) {
+  if (m <= 0 || n <= 0 || k <= 0) return 0;
+  const int tiles = ((m + Q_BM - 1) / Q_BM) * ((n + Q_BN - 1) / Q_BN);
+  hipLaunchKernelGGL((k_igemm<AF, BF, EPI>), dim3(tiles), dim3(Q_THREADS), 0, current_stream(), m, n, k, A, B, C,
+                     row_scale, lda, ldb, ldc, rowStats, colStats, bias);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error((int)e, "igemmlt launch"); return 1; }
+  return 0;
+}
+
+// ============================================================================ extract outliers
+// out is row-major [rows, idx_size]: out[r * idx_size + j] = B_fmt[r, idx[j]]  (kernel_quant.cpp:3992-4052)
+template <int F>
+__global__ void k_extract_outliers(const int8_t* __restrict__ A, const int* __restrict__ idx, int8_t* __restrict__ out,
+                                   int idx_size, int rows, int cols) {
+  const int c_out = blockIdx.x;
+  if (c_out >= idx_size) return;
+  const long long ld = (F == TURING) ? 32 * pad_to(rows, 8) : 32 * pad_to(rows, 32);
+  const int col = idx[c_out];
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) out[(long long)r * idx_size + c_out] = A[fmt_offset<F>(r, col, ld)];
+}
+
+}  // namespace bnb
+
+using namespace bnb;
+
+extern "C" {
+
+void cget_col_row_stats(fp16_t* A, float* rowStats, float* colStats, int* nnz_count_row, float nnz_threshold, int rows,
+                        int cols) {
+  if (rows <= 0 || cols <= 0) return;
+  const int col_tiles = (cols + 255) / 256, row_tiles = (rows + 15) / 16;
+  const bool vec = (((uintptr_t)A & 15) == 0) && (cols % 8 == 0);
+  if (nnz_threshold > 0.0f && nnz_count_row != nullptr)
+    hipLaunchKernelGGL(k_colrow_stats<true>, dim3(row_tiles * col_tiles), dim3(256), 0, current_stream(), A, rowStats,
+                       colStats, nnz_count_row, nnz_threshold, rows, cols, col_tiles, vec);
+  else
+    hipLaunchKernelGGL(k_colrow_stats<false>, dim3(row_tiles * col_tiles), dim3(256), 0, current_stream(), A, rowStats,
+                       colStats, nnz_count_row, nnz_threshold, rows, cols, col_tiles, vec);
+  BNB_LAUNCH_CHECK("get_col_row_stats");
+}
+
+void cdouble_rowcol_quant(fp16_t* A, float* rowStats, float* colStats, char* out_col_normed, char* out_row_normed,
+                          int* rowidx, int* colidx, fp16_t* val, int* nnz_row_ptr, float threshold, int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return;
+  const int col_tiles = (cols + 255) / 256, row_tiles = (rows + 15) / 16;
+  const bool vec = (((uintptr_t)A & 15) == 0) && (cols % 8 == 0) && (((uintptr_t)out_col_normed & 7) == 0) &&
+                   (((uintptr_t)out_row_normed & 7) == 0);
+  if (threshold > 0.0f && rowidx && colidx && val && nnz_row_ptr)
+    hipLaunchKernelGGL(k_double_rowcol_quant<true>, dim3(row_tiles * col_tiles), dim3(256), 0, current_stream(), A,
+                       rowStats, colStats, (int8_t*)out_col_normed, (int8_t*)out_row_normed, rowidx, colidx, val,
+                       nnz_row_ptr, threshold, rows, cols, col_tiles, vec);
+  else
+    hipLaunchKernelGGL(k_double_rowcol_quant<false>, dim3(row_tiles * col_tiles), dim3(256), 0, current_stream(), A,
+                       rowStats, colStats, (int8_t*)out_col_normed, (int8_t*)out_row_normed, rowidx, colidx, val,
+                       nnz_row_ptr, threshold, rows, cols, col_tiles, vec);
+  BNB_LAUNCH_CHECK("double_rowcol_quant");
+}
+
+void ctransform_row2col32(char* A, char* out, int rows, int cols) { launch_transform<COL32, false, false>((int8_t*)A, (int8_t*)out, rows, cols); }
+void ctransform_row2col32T(char* A, char* out, int rows, int cols) { launch_transform<COL32, true, false>((int8_t*)A, (int8_t*)out, rows, cols); }
+void ctransform_row2turing(char* A, char* out, int rows, int cols) { launch_transform<TURING, false, false>((int8_t*)A, (int8_t*)out, rows, cols); }
+void ctransform_row2turingT(char* A, char* out, int rows, int cols) { launch_transform<TURING, true, false>((int8_t*)A, (int8_t*)out, rows, cols); }
+void ctransform_row2ampere(char* A, char* out, int rows, int cols) { launch_transform<AMPERE, false, false>((int8_t*)A, (int8_t*)out, rows, cols); }
+void ctransform_row2ampereT(char* A, char* out, int rows, int cols) { launch_transform<AMPERE, true, false>((int8_t*)A, (int8_t*)out, rows, cols); }
+// inverse transforms (out is the row-major rows x cols matrix)
+void ctransform_col322row(char* A, char* out, int rows, int cols) { launch_transform<COL32, false, true>((int8_t*)A, (int8_t*)out, rows, cols); }
+void ctransform_turing2row(char* A, char* out, int rows, int cols) { launch_transform<TURING, false, true>((int8_t*)A, (int8_t*)out, rows, cols); }
+void ctransform_ampere2row(char* A, char* out, int rows, int cols) { launch_transform<AMPERE, false, true>((int8_t*)A, (int8_t*)out, rows, cols); }
+
+int cigemmlt_turing_32(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  return launch_igemm<COL32, TURING, EPI_I32_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
+}
+int cigemmlt_turing_8(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  return launch_igemm<COL32, TURING, EPI_I8_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
+}
+int cigemmlt_turing_8_rowscale(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  return launch_igemm<COL32, TURING, EPI_I8_COL32_ROWSCALE>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
+}
+int cigemmlt_ampere_32(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  return launch_igemm<COL32, AMPERE, EPI_I32_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
+}
+int cigemmlt_ampere_8(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  return launch_igemm<COL32, AMPERE, EPI_I8_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
+}
+int cigemmlt_ampere_8_rowscale(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  return launch_igemm<COL32, AMPERE, EPI_I8_COL32_ROWSCALE>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
+}
+
+// Additive fast path: row-major int8 A [m, k] (lda) and B [n, k] (ldb); epilogue = mm_dequant to fp16
+// row-major out [m, n] (ldc), i.e. igemmlt + cdequant_mm_int32_fp16 fused into one launch.
+int cigemmlt_row_dequant_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, fp16_t* out, const float* rowStats,
+                              const float* colStats, const fp16_t* bias, int lda, int ldb, int ldc) {
+  return launch_igemm<ROW, ROW, EPI_F16_ROW_DEQUANT>(m, n, k, A, B, out, nullptr, lda, ldb, ldc, rowStats, colStats, bias);
+}
+// Additive: row-major int8 GEMM with int32 row-major output (exact igemm, test_matmulqlt.py:194-204).
+int cigemm_row_i32(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc) {
+  return launch_igemm<ROW, ROW, EPI_I32_ROW>(m, n, k, A, B, out, nullptr, lda, ldb, ldc);
+}
+
+void cdequant_mm_int32_fp16(int* A, float* rowStats, float* colStats, fp16_t* out, float* newRowStats,
+                            float* newcolStats, fp16_t* bias, int numRows, int numCols) {
+  (void)newRowStats; (void)newcolStats;   // unused by the reference kernel as well
+  if (numRows <= 0 || numCols <= 0) return;
+  const long long groups = (long long)numRows * ((numCols + 3) / 4);
+  long long g = (groups + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_dequant_mm_col32, dim3((unsigned)g), dim3(256), 0, current_stream(), A, rowStats, colStats, out, bias,
+                     numRows, numCols);
+  BNB_LAUNCH_CHECK("dequant_mm_int32_fp16");
+}
+
+void cextractOutliers_turing(char* A, int* idx, char* out, int idx_size, int rows, int cols) {
+  if (idx_size <= 0) return;
+  hipLaunchKernelGGL(k_extract_outliers<TURING>, dim3(idx_size), dim3(256), 0, current_stream(), (int8_t*)A, idx,
+                     (int8_t*)out, idx_size, rows, cols);
+  BNB_LAUNCH_CHECK("extract_outliers");
+}
+void cextractOutliers_ampere(char* A, int* idx, char* out, int idx_size, int rows, int cols) {
+  if (idx_size <= 0) return;
+  hipLaunchKernelGGL(k_extract_outliers<AMPERE>, dim3(idx_size), dim3(256), 0, current_stream(), (int8_t*)A, idx,
+                     (int8_t*)out, idx_size, rows, cols);
+  BNB_LAUNCH_CHECK("extract_outliers");
+}
+
+}  // extern "C"

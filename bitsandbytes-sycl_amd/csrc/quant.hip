@@ -1,0 +1,428 @@
+// Blockwise quantize / dequantize for gfx950.
+//
+// Replaces (same C-ABI names, argument order and meaning):
+//   cquantize_blockwise_{fp16,bf16,fp32}{,_fp4,_nf4}     ref:sycl/pythonInterface.cpp:203-217
+//   cdequantize_blockwise_{fp16,bf16,fp32}{,_fp4,_nf4}   ref:sycl/pythonInterface.cpp:199-221
+//   cquantize_blockwise_cpu_fp32 / cdequantize_blockwise_cpu_fp32   ref:sycl/pythonInterface.cpp:419-420
+// Semantics: kQuantizeBlockwise ref:sycl/sycl_code/kernel_quant.cpp:1229-1365 and
+// kDequantizeBlockwise 1370-1471 with the intended full-size behaviour.
+//
+// Layout in HBM: A is n contiguous elements; absmax is fp32[ceil(n/bs)]; 4-bit output is
+// ceil(n/2) bytes (high nibble = even element), 8-bit output is n bytes.
+//
+// Design (MI355X): quantize is one pass, 8 elements per lane, one quantisation block per
+// 8..512 contiguous lanes; the per-block absmax is a wave64 xor-shuffle reduction (plus an
+// LDS combine across waves for bs >= 1024).  Dequantize streams 16 packed bytes per lane
+// (one 16-B load) through a 256-entry LDS pair table (byte -> two code values) and writes
+// 16-B vector stores: it is HBM-bound (roofline: 0.5 B in + 2 B out per bf16 element).
+#include "common.hpp"
+
+namespace bnb {
+
+// ============================================================================ quantize
+
+template <typename T> struct Load8;
+template <> struct Load8<float> {
+  __device__ static __forceinline__ void load(const float* p, float (&v)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+};
+template <> struct Load8<fp16_t> {
+  __device__ static __forceinline__ void load(const fp16_t* p, float (&v)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[i] & 0xFFFF));
+      v[2 * i + 1] = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[i] >> 16));
+    }
+  }
+};
+template <> struct Load8<bf16_t> {
+  __device__ static __forceinline__ void load(const bf16_t* p, float (&v)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+  }
+};
+
+// THREADS lanes per CTA, 8 elements per lane; a quantisation block spans BS/8 lanes.
+template <typename T, int BS, int DT, bool VEC>
+__global__ void __launch_bounds__((BS / 8 > 256 ? BS / 8 : 256))
+k_quantize_blockwise(const float* __restrict__ code, const T* __restrict__ A, float* __restrict__ absmax,
+                     uint8_t* __restrict__ out, long long n) {
+  constexpr int THREADS = (BS / 8 > 256 ? BS / 8 : 256);
+  constexpr int G = BS / 8;                         // lanes per quantisation block
+  constexpr int PER_CTA = THREADS * 8;
+  __shared__ float s_code[256];
+  __shared__ float s_wmax[THREADS / 64];
+  if constexpr (DT == GENERAL8BIT) {
+    for (int i = threadIdx.x; i < 256; i += THREADS) s_code[i] = code[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  for (long long base = (long long)blockIdx.x * PER_CTA; base < n; base += (long long)gridDim.x * PER_CTA) {
+    const long long e0 = base + (long long)threadIdx.x * 8;
+    float v[8];
+    if (VEC && e0 + 8 <= n) {
+      Load8<T>::load(A + e0, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (e0 + j < n) ? Io<T>::to_f32(A[e0 + j]) : 0.0f;  // fill 0
+    }
+    float m = -3.402823466e+38f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+    if constexpr (G <= 64) {
+      m = wave_max_xor(m, G);
+    } else {
+      m = wave_max_xor(m, 64);
+      if (lane == 0) s_wmax[wave] = m;
+      __syncthreads();
+      constexpr int WPB = G / 64;                    // waves per quantisation block
+      const int first = (wave / WPB) * WPB;
+      m = s_wmax[first];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) m = fmaxf(m, s_wmax[first + w]);
+      __syncthreads();
+    }
+    const long long blk = e0 / BS;
+    if ((threadIdx.x % G) == 0 && e0 < n) absmax[blk] = m;
+    const float r = 1.0f / m;                        // IEEE reciprocal (kernel_quant.cpp:1304)
+    if constexpr (DT == GENERAL8BIT) {
+      uint32_t q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = quantize_dynamic8(s_code, __fmul_rn(v[j], r));
+      if (VEC && e0 + 8 <= n) {
+        uint2 w;
+        w.x = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
+        w.y = q[4] | (q[5] << 8) | (q[6] << 16) | (q[7] << 24);
+        *reinterpret_cast<uint2*>(out + e0) = w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (e0 + j < n) out[e0 + j] = (uint8_t)q[j];
+      }
+    } else {
+      uint32_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t hi = quant4<DT>(__fmul_rn(v[2 * j], r));
+        const uint32_t lo = quant4<DT>(__fmul_rn(v[2 * j + 1], r));
+        packed |= ((hi << 4) | lo) << (8 * j);
+      }
+      const long long b0 = e0 / 2;
+      const long long nbytes = (n + 1) / 2;
+      if (VEC && b0 + 4 <= nbytes) {
+        *reinterpret_cast<uint32_t*>(out + b0) = packed;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (b0 + j < nbytes) out[b0 + j] = (uint8_t)(packed >> (8 * j));
+      }
+    }
+  }
+}
+
+// ============================================================================ dequantize
+
+template <typename T> struct Store;
+template <> struct Store<bf16_t> {
+  // 16 values -> 32 bytes
+  __device__ static __forceinline__ void store16(bf16_t* p, const float (&v)[16]) {
+    uint4 a, b;
+    a.x = pack_bf16x2(v[0], v[1]);   a.y = pack_bf16x2(v[2], v[3]);
+    a.z = pack_bf16x2(v[4], v[5]);   a.w = pack_bf16x2(v[6], v[7]);
+    b.x = pack_bf16x2(v[8], v[9]);   b.y = pack_bf16x2(v[10], v[11]);
+    b.z = pack_bf16x2(v[12], v[13]); b.w = pack_bf16x2(v[14], v[15]);
+    reinterpret_cast<uint4*>(p)[0] = a;
+    reinterpret_cast<uint4*>(p)[1] = b;
+  }
+};
+template <> struct Store<fp16_t> {
+  __device__ static __forceinline__ uint32_t pk(float a, float b) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, Io<fp16_t>::from_f32(a)) |
+           ((uint32_t)__builtin_bit_cast(uint16_t, Io<fp16_t>::from_f32(b)) << 16);
+  }
+  __device__ static __forceinline__ void store16(fp16_t* p, const float (&v)[16]) {
+    uint4 a, b;
+    a.x = pk(v[0], v[1]);   a.y = pk(v[2], v[3]);   a.z = pk(v[4], v[5]);   a.w = pk(v[6], v[7]);
+    b.x = pk(v[8], v[9]);   b.y = pk(v[10], v[11]); b.z = pk(v[12], v[13]); b.w = pk(v[14], v[15]);
+    reinterpret_cast<uint4*>(p)[0] = a;
+    reinterpret_cast<uint4*>(p)[1] = b;
+  }
+};
+template <> struct Store<float> {
+  __device__ static __forceinline__ void store16(float* p, const float (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      reinterpret_cast<float4*>(p)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+  }
+};
+
+// Each lane owns 16 packed bytes.  4-bit: 32 elements; 8-bit: 16 elements.  bs >= 64
+// guarantees one absmax per lane chunk.  The LDS table maps a byte to its code value(s).
+template <typename T, int DT, bool VEC>
+__global__ void __launch_bounds__(256)
+k_dequantize_blockwise(const float* __restrict__ code, const uint8_t* __restrict__ A,
+                       const float* __restrict__ absmax, T* __restrict__ out, int bs_shift, long long n) {
+  __shared__ float2 s_pair[256];
+  __shared__ float s_code[256];
+  {
+    const int b = threadIdx.x;
+    if constexpr (DT == GENERAL8BIT) {
+      s_code[b] = code[b];
+    } else {
+      s_pair[b] = make_float2(code4_value<DT>((uint32_t)b >> 4), code4_value<DT>((uint32_t)b & 15));
+    }
+  }
+  __syncthreads();
+  constexpr int EPL = (DT == GENERAL8BIT) ? 16 : 32;   // elements per lane
+  const long long nbytes = (DT == GENERAL8BIT) ? n : (n + 1) / 2;
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t * 16 < nbytes; t += stride) {
+    const long long byte0 = t * 16;
+    const long long e0 = t * EPL;
+    const float am = absmax[e0 >> bs_shift];
+    if (VEC && e0 + EPL <= n) {
+      const uint4 u = *reinterpret_cast<const uint4*>(A + byte0);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+      if constexpr (DT == GENERAL8BIT) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = __fmul_rn(s_code[(w[i >> 2] >> (8 * (i & 3))) & 0xFF], am);
+        Store<T>::store16(out + e0, v);
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v[16];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float2 p = s_pair[(w[2 * h + (i >> 2)] >> (8 * (i & 3))) & 0xFF];
+            v[2 * i] = __fmul_rn(p.x, am);
+            v[2 * i + 1] = __fmul_rn(p.y, am);
+          }
+          Store<T>::store16(out + e0 + 16 * h, v);
+        }
+      }
+    } else {
+      for (int i = 0; i < 16; ++i) {
+        const long long bi = byte0 + i;
+        if (bi >= nbytes) break;
+        const uint32_t byte = A[bi];
+        if constexpr (DT == GENERAL8BIT) {
+          out[bi] = Io<T>::from_f32(__fmul_rn(s_code[byte], absmax[bi >> bs_shift]));
+        } else {
+          const long long e = 2 * bi;
+          const float2 p = s_pair[byte];
+          out[e] = Io<T>::from_f32(__fmul_rn(p.x, absmax[e >> bs_shift]));
+          if (e + 1 < n) out[e + 1] = Io<T>::from_f32(__fmul_rn(p.y, absmax[(e + 1) >> bs_shift]));
+        }
+      }
+    }
+  }
+}
+
+// ============================================================================ CPU-path semantics
+// The reference's host-pointer functions (cpu_ops.cpp).  Here they are executed on the GPU:
+// host buffers are staged into HBM, processed by the kernels below, and copied back.
+
+__global__ void k_quantize_cpu_semantics(const float* __restrict__ code, const float* __restrict__ A,
+                                         float* __restrict__ absmax, uint8_t* __restrict__ out,
+                                         long long blocksize, long long n) {
+  // one workgroup per quantisation block (any blocksize): absmax = fmax over |A| from -FLT_MAX;
+  // z = A / absmax (division: common.cpp:21); left neighbour + strictly-closer-right rule.
+  __shared__ float s_code[256];
+  __shared__ float s_red[4];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_code[i] = code[i];
+  if (threadIdx.x == 0) s_code[0] = -1.0f;   // cpu_ops.cpp:20
+  const long long b0 = (long long)blockIdx.x * blocksize;
+  const long long b1 = (b0 + blocksize < n) ? b0 + blocksize : n;
+  float m = -3.402823466e+38f;
+  for (long long i = b0 + threadIdx.x; i < b1; i += blockDim.x) m = fmaxf(m, fabsf(A[i]));
+  m = wave_max_xor(m, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
+  if (threadIdx.x == 0) absmax[blockIdx.x] = m;
+  for (long long i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
+    const float z = __fdiv_rn(A[i], m);
+    int lo = 0, hi = 256;   // upper_bound
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_code[mid] <= z) lo = mid + 1; else hi = mid;
+    }
+    int idx = lo - 1;
+    if (idx < 0 || z != z) idx = 0;
+    if (idx < 255) {
+      const float dl = fabsf(__fsub_rn(z, s_code[idx]));
+      const float dr = fabsf(__fsub_rn(z, s_code[idx + 1]));
+      if (dr < dl) idx += 1;
+    }
+    out[i] = (uint8_t)idx;
+  }
+}
+
+__global__ void k_dequantize_cpu_semantics(const float* __restrict__ code, const uint8_t* __restrict__ A,
+                                           const float* __restrict__ absmax, float* __restrict__ out,
+                                           long long blocksize, long long n) {
+  __shared__ float s_code[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_code[i] = code[i];
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = __fmul_rn(s_code[A[i]], absmax[i / blocksize]);
+}
+
+// ============================================================================ launchers
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static inline int stream_grid(long long work_items, int threads) {
+  long long g = (work_items + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > 8192) g = 8192;
+  return (int)g;
+}
+
+template <typename T, int DT, int BS>
+static void launch_quant_bs(const float* code, const T* A, float* absmax, uint8_t* out, long long n, bool vec) {
+  constexpr int THREADS = (BS / 8 > 256 ? BS / 8 : 256);
+  const int grid = stream_grid((n + 7) / 8, THREADS);
+  if (vec)
+    hipLaunchKernelGGL((k_quantize_blockwise<T, BS, DT, true>), dim3(grid), dim3(THREADS), 0, current_stream(), code, A, absmax, out, n);
+  else
+    hipLaunchKernelGGL((k_quantize_blockwise<T, BS, DT, false>), dim3(grid), dim3(THREADS), 0, current_stream(), code, A, absmax, out, n);
+}
+
+template <typename T, int DT>
+void quantize_blockwise(const float* code, const T* A, float* absmax, uint8_t* out, int blocksize, long long n) {
+  if (n <= 0) return;
+  const bool vec = aligned16(A) && ((uintptr_t)out & 7) == 0;
+  switch (blocksize) {
+    case 4096: launch_quant_bs<T, DT, 4096>(code, A, absmax, out, n, vec); break;
+    case 2048: launch_quant_bs<T, DT, 2048>(code, A, absmax, out, n, vec); break;
+    case 1024: launch_quant_bs<T, DT, 1024>(code, A, absmax, out, n, vec); break;
+    case 512: launch_quant_bs<T, DT, 512>(code, A, absmax, out, n, vec); break;
+    case 256: launch_quant_bs<T, DT, 256>(code, A, absmax, out, n, vec); break;
+    case 128: launch_quant_bs<T, DT, 128>(code, A, absmax, out, n, vec); break;
+    case 64: launch_quant_bs<T, DT, 64>(code, A, absmax, out, n, vec); break;
+    default: set_error(1, "quantize_blockwise: unsupported blocksize"); return;
+  }
+  BNB_LAUNCH_CHECK("quantize_blockwise");
+}
+
+template <typename T, int DT>
+void dequantize_blockwise(const float* code, const uint8_t* A, const float* absmax, T* out, int blocksize, long long n) {
+  if (n <= 0) return;
+  if (blocksize < 64 || (blocksize & (blocksize - 1))) { set_error(1, "dequantize_blockwise: unsupported blocksize"); return; }
+  const long long nbytes = (DT == GENERAL8BIT) ? n : (n + 1) / 2;
+  const int grid = stream_grid((nbytes + 15) / 16, 256);
+  const bool vec = aligned16(A) && aligned16(out);
+  if (vec)
+    hipLaunchKernelGGL((k_dequantize_blockwise<T, DT, true>), dim3(grid), dim3(256), 0, current_stream(), code, A, absmax, out, __builtin_ctz(blocksize), n);
+  else
+    hipLaunchKernelGGL((k_dequantize_blockwise<T, DT, false>), dim3(grid), dim3(256), 0, current_stream(), code, A, absmax, out, __builtin_ctz(blocksize), n);
+  BNB_LAUNCH_CHECK("dequantize_blockwise");
+}
+
+}  // namespace bnb
+
+using namespace bnb;
+
+// ============================================================================ C-ABI
+extern "C" {
+
+#define BNB_QUANT_ABI(fname, T, DT)                                                                   \
+  void fname(float* code, T* A, float* absmax, unsigned char* out, int blocksize, const int n) {     \
+    quantize_blockwise<T, DT>(code, A, absmax, out, blocksize, n);                                    \
+  }
+#define BNB_DEQUANT_ABI(fname, T, DT)                                                                 \
+  void fname(float* code, unsigned char* A, float* absmax, T* out, int blocksize, const int n) {     \
+    dequantize_blockwise<T, DT>(code, A, absmax, out, blocksize, n);                                  \
+  }
+
+BNB_QUANT_ABI(cquantize_blockwise_fp16, fp16_t, GENERAL8BIT)
+BNB_QUANT_ABI(cquantize_blockwise_fp16_fp4, fp16_t, FP4)
+BNB_QUANT_ABI(cquantize_blockwise_fp16_nf4, fp16_t, NF4)
+BNB_QUANT_ABI(cquantize_blockwise_bf16, bf16_t, GENERAL8BIT)
+BNB_QUANT_ABI(cquantize_blockwise_bf16_fp4, bf16_t, FP4)
+BNB_QUANT_ABI(cquantize_blockwise_bf16_nf4, bf16_t, NF4)
+BNB_QUANT_ABI(cquantize_blockwise_fp32, float, GENERAL8BIT)
+BNB_QUANT_ABI(cquantize_blockwise_fp32_fp4, float, FP4)
+BNB_QUANT_ABI(cquantize_blockwise_fp32_nf4, float, NF4)
+
+BNB_DEQUANT_ABI(cdequantize_blockwise_fp16, fp16_t, GENERAL8BIT)
+BNB_DEQUANT_ABI(cdequantize_blockwise_fp16_fp4, fp16_t, FP4)
+BNB_DEQUANT_ABI(cdequantize_blockwise_fp16_nf4, fp16_t, NF4)
+BNB_DEQUANT_ABI(cdequantize_blockwise_bf16, bf16_t, GENERAL8BIT)
+BNB_DEQUANT_ABI(cdequantize_blockwise_bf16_fp4, bf16_t, FP4)
+BNB_DEQUANT_ABI(cdequantize_blockwise_bf16_nf4, bf16_t, NF4)
+BNB_DEQUANT_ABI(cdequantize_blockwise_fp32, float, GENERAL8BIT)
+BNB_DEQUANT_ABI(cdequantize_blockwise_fp32_fp4, float, FP4)
+BNB_DEQUANT_ABI(cdequantize_blockwise_fp32_nf4, float, NF4)
+
+// Host-pointer entry points (ref:sycl/pythonInterface.cpp:419-420).  Executed on the current
+// GPU: stage -> kernel -> copy back (synchronous, like the reference CPU path).
+void cquantize_blockwise_cpu_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize,
+                                  long long n) {
+  if (n <= 0 || blocksize <= 0) return;
+  const long long nb = (n + blocksize - 1) / blocksize;
+  float *d_code = nullptr, *d_A = nullptr, *d_absmax = nullptr;
+  uint8_t* d_out = nullptr;
+  hipStream_t s = current_stream();
+  if (hipMalloc(&d_code, 256 * sizeof(float)) != hipSuccess || hipMalloc(&d_A, n * sizeof(float)) != hipSuccess ||
+      hipMalloc(&d_absmax, nb * sizeof(float)) != hipSuccess || hipMalloc(&d_out, n) != hipSuccess) {
+    set_error(2, "cquantize_blockwise_cpu_fp32: hipMalloc failed");
+  } else {
+    code[0] = -1.0f;   // documented in-place side effect of the reference (cpu_ops.cpp:20)
+    hipMemcpyAsync(d_code, code, 256 * sizeof(float), hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_A, A, n * sizeof(float), hipMemcpyHostToDevice, s);
+    hipLaunchKernelGGL(k_quantize_cpu_semantics, dim3((unsigned)nb), dim3(256), 0, s, d_code, d_A, d_absmax, d_out, blocksize, n);
+    BNB_LAUNCH_CHECK("quantize_cpu_semantics");
+    hipMemcpyAsync(absmax, d_absmax, nb * sizeof(float), hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+  }
+  hipFree(d_code); hipFree(d_A); hipFree(d_absmax); hipFree(d_out);
+}
+
+void cdequantize_blockwise_cpu_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize,
+                                    long long n) {
+  if (n <= 0 || blocksize <= 0) return;
+  const long long nb = (n + blocksize - 1) / blocksize;
+  float *d_code = nullptr, *d_absmax = nullptr, *d_out = nullptr;
+  uint8_t* d_A = nullptr;
+  hipStream_t s = current_stream();
+  if (hipMalloc(&d_code, 256 * sizeof(float)) != hipSuccess || hipMalloc(&d_A, n) != hipSuccess ||
+      hipMalloc(&d_absmax, nb * sizeof(float)) != hipSuccess || hipMalloc(&d_out, n * sizeof(float)) != hipSuccess) {
+    set_error(2, "cdequantize_blockwise_cpu_fp32: hipMalloc failed");
+  } else {
+    hipMemcpyAsync(d_code, code, 256 * sizeof(float), hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_A, A, n, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_absmax, absmax, nb * sizeof(float), hipMemcpyHostToDevice, s);
+    hipLaunchKernelGGL(k_dequantize_cpu_semantics, dim3(stream_grid(n, 256)), dim3(256), 0, s, d_code, d_A, d_absmax, d_out, blocksize, n);
+    BNB_LAUNCH_CHECK("dequantize_cpu_semantics");
+    hipMemcpyAsync(out, d_out, n * sizeof(float), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+  }
+  hipFree(d_code); hipFree(d_A); hipFree(d_absmax); hipFree(d_out);
+}
+
+// Device-resident variant of the CPU-path dequantize (one byte per element, any blocksize);
+// used by the config-1 GPU measurement.  Not in the reference ABI.
+void cdequantize_blockwise_bytes_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize,
+                                      long long n) {
+  if (n <= 0 || blocksize <= 0) return;
+  hipLaunchKernelGGL(k_dequantize_cpu_semantics, dim3(stream_grid(n, 256)), dim3(256), 0, current_stream(), code, A,
+                     absmax, out, blocksize, n);
+  BNB_LAUNCH_CHECK("dequantize_bytes");
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+"""ctypes loader for the gfx950 C-ABI library (replaces ref:python_src_quants/cextension.py:43-129).
+
+The library is built in-tree (``bitsandbytes-sycl_amd/csrc`` -> ``libbitsandbytes_hip.so``
+next to this file).  There is no CPU fallback: if the library is missing, ``lib`` is a
+stub whose every attribute access raises, so GPU ops fail loudly instead of silently
+running something else.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import logging
+import os
+from pathlib import Path
+
+logger = logging.getLogger(__name__)
+
+PACKAGE_DIR = Path(__file__).parent
+LIBRARY_NAME = "libbitsandbytes_hip.so"
+
+
+def get_hip_bnb_library_path() -> Path:
+    override = os.environ.get("BNB_HIP_LIBRARY")
+    return Path(override) if override else PACKAGE_DIR / LIBRARY_NAME
+
+
+class BNBNativeLibrary:
+    _lib: ct.CDLL
+    compiled_with_hip = True
+
+    def __init__(self, lib: ct.CDLL):
+        self._lib = lib
+        # restypes the reference sets at load (cextension.py:82-84) + the additive entry points
+        lib.get_context.restype = ct.c_void_p
+        lib.get_cusparse.restype = ct.c_void_p
+        lib.cget_managed_ptr.restype = ct.c_void_p
+        lib.cget_stream.restype = ct.c_void_p
+        lib.cget_last_error_message.restype = ct.c_char_p
+        for name in ("cigemmlt_turing_32", "cigemmlt_turing_8", "cigemmlt_turing_8_rowscale",
+                     "cigemmlt_ampere_32", "cigemmlt_ampere_8", "cigemmlt_ampere_8_rowscale",
+                     "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cget_last_error", "cget_abi_version"):
+            getattr(lib, name).restype = ct.c_int
+
+    def __getattr__(self, item):
+        return getattr(self._lib, item)
+
+
+class _MissingLibrary:
+    def __init__(self, err: Exception):
+        self._err = err
+
+    def __getattr__(self, item):
+        raise RuntimeError(
+            f"bitsandbytes HIP library not loaded ({self._err}); build it with "
+            f"`make -C bitsandbytes-sycl_amd/csrc` (gfx950). There is no CPU fallback."
+        )
+
+    def __bool__(self):
+        return False
+
+
+def get_native_library():
+    path = get_hip_bnb_library_path()
+    dll = ct.cdll.LoadLibrary(str(path))
+    if not hasattr(dll, "get_context"):
+        raise RuntimeError(f"{path} does not export the bitsandbytes C-ABI")
+    return BNBNativeLibrary(dll)
+
+
+try:
+    lib = get_native_library()
+    HIP_AVAILABLE = True
+except Exception as e:  # noqa: BLE001 - reported loudly on first use
+    lib = _MissingLibrary(e)
+    HIP_AVAILABLE = False
+    logger.error("Could not load the bitsandbytes HIP library: %s", e)

@@ -1,0 +1,816 @@
+"""Functional surface of the quantized-matmul hot path, MI355X backend.
+
+Mirrors ref:python_src_quants/functional.py for the hot-path functions (same names, argument
+meaning, returned shapes/dtypes and error behaviour) with device type ``"cuda"`` (ROCm)
+instead of ``"xpu"``.  Every GPU op crosses into the gfx950 C-ABI library through ctypes;
+there is no CPU/torch fallback for them.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from functools import reduce
+import operator
+from typing import Any, Dict, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from .cextension import lib
+from .utils import pack_dict_to_tensor, unpack_tensor_to_dict
+
+name2qmap: Dict[str, Tensor] = {}
+
+dtype2bytes = {torch.float32: 4, torch.float16: 2, torch.bfloat16: 2, torch.uint8: 1, torch.int8: 1}
+
+_BLOCKSIZES = [4096, 2048, 1024, 512, 256, 128, 64]
+
+
+def prod(iterable):
+    return reduce(operator.mul, iterable, 1)
+
+
+# ----------------------------------------------------------------------------- quantisation maps
+def create_linear_map(signed=True, total_bits=8, add_zero=True):
+    """ref:functional.py:248-264"""
+    sign = -1.0 if signed else 0.0
+    total_values = 2**total_bits
+    if add_zero or total_bits < 8:
+        total_values = 2**total_bits if not signed else 2**total_bits - 1
+    values = torch.linspace(sign, 1.0, total_values)
+    gap = 256 - values.numel()
+    if gap == 0:
+        return values
+    half = values.numel() // 2
+    return torch.Tensor(values[:half].tolist() + [0] * gap + values[half:].tolist())
+
+
+def create_normal_map(offset=0.9677083, use_extra_value=True):
+    """ref:functional.py:267-294 (needs scipy)."""
+    from scipy.stats import norm
+
+    if use_extra_value:
+        v1 = norm.ppf(torch.linspace(offset, 0.5, 9)[:-1]).tolist()
+        v2 = [0] * (256 - 15)
+        v3 = (-norm.ppf(torch.linspace(offset, 0.5, 8)[:-1])).tolist()
+    else:
+        v1 = norm.ppf(torch.linspace(offset, 0.5, 8)[:-1]).tolist()
+        v2 = [0] * (256 - 14)
+        v3 = (-norm.ppf(torch.linspace(offset, 0.5, 8)[:-1])).tolist()
+    values = torch.Tensor(v1 + v2 + v3).sort().values
+    values /= values.max()
+    assert values.numel() == 256
+    return values
+
+
+def create_dynamic_map(signed=True, max_exponent_bits=7, total_bits=8):
+    """Dynamic exponent/fraction 8-bit map, ref:functional.py:339-391."""
+    data = []
+    non_sign_bits = total_bits - 1
+    additional_items = 2 ** (non_sign_bits - max_exponent_bits) - 1
+    for i in range(max_exponent_bits):
+        fraction_items = int(
+            2 ** (i + non_sign_bits - max_exponent_bits) + 1
+            if signed
+            else 2 ** (i + non_sign_bits - max_exponent_bits + 1) + 1,
+        )
+        boundaries = torch.linspace(0.1, 1, fraction_items)
+        means = (boundaries[:-1] + boundaries[1:]) / 2.0
+        data += ((10 ** (-(max_exponent_bits - 1) + i)) * means).tolist()
+        if signed:
+            data += (-(10 ** (-(max_exponent_bits - 1) + i)) * means).tolist()
+    if additional_items > 0:
+        boundaries = torch.linspace(0.1, 1, additional_items + 1)
+        means = (boundaries[:-1] + boundaries[1:]) / 2.0
+        data += ((10 ** (-(max_exponent_bits - 1) + max_exponent_bits - 1)) * means).tolist()
+        if signed:
+            data += (-(10 ** (-(max_exponent_bits - 1) + max_exponent_bits - 1)) * means).tolist()
+    data.append(0)
+    data.append(1.0)
+    assert len(data) == 2**total_bits
+    data += [0] * (256 - len(data))
+    data.sort()
+    return Tensor(data)
+
+
+def get_4bit_type(typename, device=None, blocksize=64):
+    """16-entry 4-bit code tables, ref:functional.py:1020-1099."""
+    if device is None:
+        device = "cuda"
+    if typename == "nf4":
+        data = [-1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453,
+                -0.28444138169288635, -0.18477343022823334, -0.09105003625154495, 0.0,
+                0.07958029955625534, 0.16093020141124725, 0.24611230194568634, 0.33791524171829224,
+                0.44070982933044434, 0.5626170039176941, 0.7229568362236023, 1.0]
+    elif typename == "fp4":
+        data = [0, 0.0625, 8.0, 12.0, 4.0, 6.0, 2.0, 3.0, -0, -0.0625, -8.0, -12.0, -4.0, -6.0, -2.0, -3.0]
+    elif typename == "int4":
+        data = [7, 6, 5, 4, 3, 2, 1, 0, -0, -1, -2, -3, -4, -5, -6, -7]
+    elif typename == "af4":
+        if blocksize != 64:
+            raise NotImplementedError("4-bit AbnormalFloats currently only support blocksize 64.")
+        data = [-1.0, -0.69441008, -0.51243739, -0.3736951, -0.25607552, -0.14982478, -0.04934812, 0.0,
+                0.04273164, 0.12934483, 0.21961274, 0.31675666, 0.42563882, 0.55496234, 0.72424863, 1.0][::-1]
+    else:
+        raise NotImplementedError(f"Typename {typename} not supported")
+    t = torch.tensor(data, device=device)
+    t.div_(t.abs().max())
+    assert t.numel() == 16
+    return t
+
+
+def _dynamic_map(device) -> Tensor:
+    """The default dynamic map, cached once per device (the CPU copy is handed out as a clone
+    because the CPU entry point rewrites code[0] in place, cpu_ops.cpp:20)."""
+    if "dynamic" not in name2qmap:
+        name2qmap["dynamic"] = create_dynamic_map()
+    device = torch.device(device)
+    if device.type == "cpu":
+        return name2qmap["dynamic"].clone()
+    key = f"dynamic@{device}"
+    if key not in name2qmap:
+        name2qmap[key] = name2qmap["dynamic"].to(device)
+    return name2qmap[key]
+
+
+def get_special_format_str():
+    """Weight tile format for igemmlt (ref:functional.py:410-418 returns 'col_turing' on XPU)."""
+    return "col_turing"
+
+
+# ----------------------------------------------------------------------------- call plumbing
+def is_on_gpu(tensors):
+    on_gpu = True
+    gpu_ids = set()
+    for t in tensors:
+        if t is None:
+            continue
+        on_gpu &= t.device.type == "cuda"
+        gpu_ids.add(t.device.index)
+    if not on_gpu:
+        raise TypeError(
+            "All input tensors need to be on the same GPU, but found some tensors to not be on a GPU:\n "
+            f"{[(t.shape, t.device) for t in tensors if t is not None]}",
+        )
+    if len(gpu_ids) > 1:
+        raise TypeError(
+            "Input tensors need to be on the same GPU, but found the following tensor and device combinations:\n "
+            f"{[(t.shape, t.device) for t in tensors if t is not None]}",
+        )
+    return on_gpu
+
+
+def get_ptr(A: Optional[Tensor]) -> Optional[ct.c_void_p]:
+    if A is None:
+        return None
+    return ct.c_void_p(A.data.data_ptr())
+
+
+def pre_call(device):
+    """Select the device (ref:functional.py:461-464) and bind the library to torch's current stream."""
+    prev_device = torch.cuda.current_device()
+    torch.cuda.set_device(device)
+    lib.cset_stream(ct.c_void_p(torch.cuda.current_stream(device).cuda_stream))
+    return prev_device
+
+
+def post_call(prev_device):
+    torch.cuda.set_device(prev_device)
+    err = lib.cget_last_error()
+    if err:
+        raise RuntimeError(f"bitsandbytes HIP kernel error: {lib.cget_last_error_message().decode()}")
+
+
+# ----------------------------------------------------------------------------- QuantState
+class QuantState:
+    """Container for quantisation state components (ref:functional.py:625-798)."""
+
+    valid_quant_types = ("fp4", "nf4")
+    valid_qs_type_keys = [f"bitsandbytes__{x}" for x in valid_quant_types]
+    valid_qs_keys = ["absmax", "quant_map", "nested_absmax", "nested_quant_map", "quant_state", "quant_type",
+                     "blocksize", "dtype", "shape", "nested_blocksize", "nested_dtype", "nested_offset"]
+
+    def __init__(self, absmax, shape=None, code=None, blocksize=None, quant_type=None, dtype=None, offset=None,
+                 state2=None):
+        self.absmax = absmax
+        self.shape = shape
+        self.code = code
+        self.dtype = dtype
+        self.blocksize = blocksize
+        self.quant_type = quant_type
+        self.offset = offset
+        self.state2 = state2
+        self.nested = state2 is not None
+
+    def __get_item__(self, idx):
+        if self.nested:
+            list_repr = [self.absmax, self.shape, self.dtype, self.blocksize, [self.offset, self.state2], self.quant_type]
+        else:
+            list_repr = [self.absmax, self.shape, self.dtype, self.blocksize, None, self.quant_type]
+        return list_repr[idx]
+
+    @classmethod
+    def from_dict(cls, qs_dict: Dict[str, Any], device: torch.device) -> "QuantState":
+        qs_key = [k for k, v in qs_dict.items() if "quant_state" in k and isinstance(v, torch.Tensor)]
+        if not len(qs_key) and "quant_type" not in qs_dict:
+            raise ValueError("Expected packed or unpacked quant_state items, found neither")
+        elif len(qs_key) != 1 or qs_key[0].split(".")[-1] not in cls.valid_qs_type_keys:
+            raise ValueError(
+                f"There should be exactly one `quant_state` item with ending from {cls.valid_qs_type_keys}.\n"
+                f"Detected {qs_key}.",
+            )
+        if len(qs_key) == 1:
+            qs_dict.update(unpack_tensor_to_dict(qs_dict.pop(qs_key[0])))
+        qs_dict = {k.split(".")[-1]: v for k, v in qs_dict.items()}
+        assert set(qs_dict.keys()).issubset(cls.valid_qs_keys)
+        if "nested_absmax" in qs_dict:
+            offset = torch.tensor(float(qs_dict["nested_offset"])).to(device)
+            state2 = cls(absmax=qs_dict["nested_absmax"].to(device), blocksize=qs_dict["nested_blocksize"],
+                         code=qs_dict["nested_quant_map"].to(device), dtype=getattr(torch, qs_dict["nested_dtype"]))
+        else:
+            offset, state2 = None, None
+        return cls(quant_type=qs_dict["quant_type"], absmax=qs_dict["absmax"].to(device),
+                   blocksize=qs_dict["blocksize"], code=qs_dict["quant_map"].to(device),
+                   dtype=getattr(torch, qs_dict["dtype"]),
+                   shape=torch.Size(qs_dict["shape"]) if qs_dict["shape"] is not None else None,
+                   offset=offset, state2=state2)
+
+    def as_dict(self, packed=False):
+        qs_dict = {
+            "quant_type": self.quant_type,
+            "absmax": self.absmax,
+            "blocksize": self.blocksize,
+            "quant_map": self.code,
+            "dtype": str(self.dtype).strip("torch."),
+            "shape": tuple(self.shape),
+        }
+        if self.nested:
+            qs_dict.update({
+                "nested_absmax": self.state2.absmax,
+                "nested_blocksize": self.state2.blocksize,
+                "nested_quant_map": self.state2.code.clone(),
+                "nested_dtype": str(self.state2.dtype).strip("torch."),
+                "nested_offset": self.offset.item(),
+            })
+        if not packed:
+            return qs_dict
+        qs_packed = {k: v for k, v in qs_dict.items() if isinstance(v, torch.Tensor)}
+        non_tensor = {k: v for k, v in qs_dict.items() if not isinstance(v, torch.Tensor)}
+        qs_packed["quant_state." + "bitsandbytes__" + self.quant_type] = pack_dict_to_tensor(non_tensor)
+        return qs_packed
+
+    def to(self, device):
+        self.absmax = self.absmax.to(device)
+        if self.nested:
+            self.offset = self.offset.to(device)
+            self.state2.absmax = self.state2.absmax.to(device)
+            self.state2.code = self.state2.code.to(device)
+
+    def __eq__(self, other):
+        if not isinstance(other, QuantState):
+            return False
+        return (
+            torch.allclose(self.absmax, other.absmax, atol=1e-6)
+            and self.shape == other.shape
+            and torch.allclose(self.code, other.code, atol=1e-6)
+            and self.dtype == other.dtype
+            and self.blocksize == other.blocksize
+            and self.quant_type == other.quant_type
+            and (self.offset == other.offset if self.offset is not None and other.offset is not None
+                 else self.offset is other.offset)
+            and (self.state2 == other.state2 if self.state2 is not None and other.state2 is not None
+                 else self.state2 is other.state2)
+        )
+
+
+# ----------------------------------------------------------------------------- 8-bit blockwise
+_QB = {torch.float32: "fp32", torch.float16: "fp16", torch.bfloat16: "bf16"}
+
+
+def quantize_blockwise(A: Tensor, code: Optional[Tensor] = None, absmax: Optional[Tensor] = None,
+                       out: Optional[Tensor] = None, blocksize=4096, nested=False) -> Tuple[Tensor, QuantState]:
+    """Blockwise dynamic 8-bit quantisation (ref:functional.py:801-918)."""
+    if code is None:
+        code = _dynamic_map(A.device)
+    if absmax is None:
+        n = A.numel()
+        blocks = n // blocksize + (1 if n % blocksize > 0 else 0)
+        absmax = torch.zeros((blocks,), device=A.device, dtype=torch.float32)
+    if out is None:
+        out = torch.zeros_like(A, dtype=torch.uint8)
+
+    if A.device.type != "cpu":
+        assert blocksize in _BLOCKSIZES
+        prev_device = pre_call(A.device)
+        code = code.to(A.device)
+        is_on_gpu([code, A, out, absmax])
+        if A.dtype not in _QB:
+            raise ValueError(f"Blockwise quantization only supports 16/32-bit floats, but got {A.dtype}")
+        fn = getattr(lib, f"cquantize_blockwise_{_QB[A.dtype]}")
+        fn(get_ptr(code), get_ptr(A), get_ptr(absmax), get_ptr(out), ct.c_int32(blocksize), ct.c_int(A.numel()))
+        post_call(prev_device)
+    else:
+        # host tensors: the reference's CPU entry point (executed by the library on the GPU)
+        code = code.cpu()
+        lib.cquantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(A), get_ptr(absmax), get_ptr(out),
+                                         ct.c_longlong(blocksize), ct.c_longlong(A.numel()))
+
+    if nested:
+        offset = absmax.mean()
+        absmax -= offset
+        qabsmax, state2 = quantize_blockwise(absmax, blocksize=blocksize, nested=False)
+        quant_state = QuantState(absmax=qabsmax, code=code, blocksize=blocksize, dtype=A.dtype, offset=offset,
+                                 state2=state2)
+    else:
+        quant_state = QuantState(absmax=absmax, code=code, blocksize=blocksize, dtype=A.dtype)
+    return out, quant_state
+
+
+def dequantize_blockwise(A: Tensor, quant_state: Optional[QuantState] = None, absmax: Optional[Tensor] = None,
+                         code: Optional[Tensor] = None, out: Optional[Tensor] = None, blocksize: int = 4096,
+                         nested=False) -> Tensor:
+    """ref:functional.py:921-1017"""
+    assert quant_state is not None or absmax is not None
+    if code is None and quant_state is None:
+        code = _dynamic_map(A.device)
+    if quant_state is None:
+        quant_state = QuantState(absmax=absmax, code=code, blocksize=blocksize, dtype=torch.float32)
+
+    absmax = quant_state.absmax
+    if quant_state.nested:
+        absmax = dequantize_blockwise(quant_state.absmax, quant_state.state2)
+        absmax += quant_state.offset
+        if absmax.dtype != torch.float32:
+            absmax = absmax.float()
+
+    if out is None:
+        out = torch.empty(A.shape, dtype=quant_state.dtype, device=A.device)
+
+    if A.device.type != "cpu":
+        prev_device = pre_call(A.device)
+        code = quant_state.code.to(A.device)
+        if quant_state.blocksize not in [2048, 4096, 1024, 512, 256, 128, 64]:
+            raise ValueError(
+                f"The blockwise of {quant_state.blocksize} is not supported. "
+                "Supported values: [2048, 4096, 1024, 512, 256, 128, 64]",
+            )
+        is_on_gpu([A, absmax, out])
+        if out.dtype not in _QB:
+            raise ValueError(f"Blockwise quantization only supports 16/32-bit floats, but got {A.dtype}")
+        fn = getattr(lib, f"cdequantize_blockwise_{_QB[out.dtype]}")
+        fn(get_ptr(code), get_ptr(A), get_ptr(absmax), get_ptr(out), ct.c_int(quant_state.blocksize),
+           ct.c_int(A.numel()))
+        post_call(prev_device)
+    else:
+        code = quant_state.code.cpu()
+        lib.cdequantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(A), get_ptr(quant_state.absmax), get_ptr(out),
+                                           ct.c_longlong(quant_state.blocksize), ct.c_longlong(A.numel()))
+    return out
+
+
+# ----------------------------------------------------------------------------- 4-bit
+def quantize_fp4(A, absmax=None, out=None, blocksize=64, compress_statistics=False, quant_storage=torch.uint8):
+    return quantize_4bit(A, absmax, out, blocksize, compress_statistics, "fp4", quant_storage)
+
+
+def quantize_nf4(A, absmax=None, out=None, blocksize=64, compress_statistics=False, quant_storage=torch.uint8):
+    return quantize_4bit(A, absmax, out, blocksize, compress_statistics, "nf4", quant_storage)
+
+
+def quantize_4bit(A: Tensor, absmax: Optional[Tensor] = None, out: Optional[Tensor] = None, blocksize=64,
+                  compress_statistics=False, quant_type="fp4",
+                  quant_storage=torch.uint8) -> Tuple[Tensor, QuantState]:
+    """Blockwise FP4/NF4 quantisation (ref:functional.py:1124-1268)."""
+    if A.device.type != "cuda":
+        raise NotImplementedError(f"Device type not supported for FP4 quantization: {A.device.type}")
+    if quant_type not in ["fp4", "nf4"]:
+        raise NotImplementedError(f"4-bit quantization data type {quant_type} is not implemented.")
+    n = A.numel()
+    input_shape = A.shape
+    if absmax is None:
+        blocks = n // blocksize + (1 if n % blocksize > 0 else 0)
+        absmax = torch.zeros((blocks,), device=A.device, dtype=torch.float32)
+    if out is None:
+        mod = dtype2bytes[quant_storage] * 2
+        out = torch.zeros(((n + 1) // mod, 1), dtype=quant_storage, device=A.device)
+    assert blocksize in _BLOCKSIZES
+
+    prev_device = pre_call(A.device)
+    is_on_gpu([A, out, absmax])
+    if A.dtype not in _QB:
+        raise ValueError(f"Blockwise quantization only supports 16/32-bit floats, but got {A.dtype}")
+    fn = getattr(lib, f"cquantize_blockwise_{_QB[A.dtype]}_{quant_type}")
+    fn(get_ptr(None), get_ptr(A), get_ptr(absmax), get_ptr(out), ct.c_int32(blocksize), ct.c_int(n))
+    post_call(prev_device)
+
+    code = get_4bit_type(quant_type, device=A.device)
+    if compress_statistics:
+        offset = absmax.mean()
+        absmax -= offset
+        qabsmax, state2 = quantize_blockwise(absmax, blocksize=256)
+        del absmax
+        state = QuantState(absmax=qabsmax, shape=input_shape, dtype=A.dtype, blocksize=blocksize, code=code,
+                           quant_type=quant_type, offset=offset, state2=state2)
+    else:
+        state = QuantState(absmax=absmax, shape=input_shape, dtype=A.dtype, blocksize=blocksize, code=code,
+                           quant_type=quant_type)
+    return out, state
+
+
+def dequantize_fp4(A, quant_state=None, absmax=None, out=None, blocksize: int = 64):
+    return dequantize_4bit(A, quant_state, absmax, out, blocksize, "fp4")
+
+
+def dequantize_nf4(A, quant_state=None, absmax=None, out=None, blocksize: int = 64):
+    return dequantize_4bit(A, quant_state, absmax, out, blocksize, "nf4")
+
+
+def _absmax_fp32(state: QuantState) -> Tensor:
+    """Per-block fp32 absmax, resolving nested statistics (ref:functional.py:1346-1350, 1982-1984)."""
+    absmax = state.absmax
+    if state.nested:
+        absmax = dequantize_blockwise(state.absmax, state.state2)
+        absmax += state.offset
+        if absmax.dtype != torch.float32:
+            absmax = absmax.float()
+    return absmax
+
+
+def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, absmax: Optional[Tensor] = None,
+                    out: Optional[Tensor] = None, blocksize: int = 64, quant_type="fp4") -> Tensor:
+    """ref:functional.py:1291-1424"""
+    if blocksize not in [2048, 4096, 1024, 512, 256, 128, 64]:
+        raise ValueError(
+            f"The blockwise of {blocksize} is not supported. Supported values: [2048, 4096, 1024, 512, 256, 128, 64]",
+        )
+    if quant_type not in ["fp4", "nf4"]:
+        raise NotImplementedError(f"4-bit quantization data type {quant_type} is not implemented.")
+    if quant_state is None:
+        assert absmax is not None and out is not None
+        quant_state = QuantState(absmax=absmax, shape=out.shape, dtype=out.dtype, blocksize=blocksize,
+                                 quant_type=quant_type)
+    else:
+        absmax = quant_state.absmax
+    if quant_state.nested:
+        absmax = _absmax_fp32(quant_state)
+    if out is None:
+        out = torch.empty(quant_state.shape, dtype=quant_state.dtype, device=A.device)
+    n = out.numel()
+
+    prev_device = pre_call(A.device)
+    is_on_gpu([A, absmax, out])
+    if out.dtype not in _QB:
+        raise ValueError(f"Blockwise quantization only supports 16/32-bit floats, but got {A.dtype}")
+    qt = "fp4" if quant_state.quant_type == "fp4" else "nf4"
+    fn = getattr(lib, f"cdequantize_blockwise_{_QB[out.dtype]}_{qt}")
+    fn(get_ptr(None), get_ptr(A), get_ptr(absmax), get_ptr(out), ct.c_int(quant_state.blocksize), ct.c_int(n))
+    post_call(prev_device)
+
+    if A.shape[0] == 1:   # is_transposed (ref:functional.py:1420-1424)
+        return out.t()
+    return out
+
+
+# ----------------------------------------------------------------------------- 4-bit matmul
+def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=False, transposed_B=False,
+              state=None):
+    """4-bit GEMV for a single activation row (ref:functional.py:1961-2060)."""
+    prev_device = pre_call(A.device)
+    if state is None:
+        raise ValueError("state cannot None. gem_4bit( ) requires the state from quantize_4bit( )")
+    if A.numel() != A.shape[-1]:
+        raise ValueError(
+            'Dimensions of A are invalid. Must be a vector with the leading dimensions of "1", e.g. [1, 1, 2048]',
+        )
+    Bshape = state.shape
+    bout = Bshape[0]
+    absmax = _absmax_fp32(state)
+    if out is None:
+        if len(A.shape) == 3:
+            out = torch.empty(size=(A.shape[0], A.shape[1], bout), dtype=A.dtype, device=A.device)
+        else:
+            out = torch.empty(size=(A.shape[0], bout), dtype=A.dtype, device=A.device)
+    m, n, k = Bshape[0], 1, Bshape[1]
+    lda, ldc, ldb = Bshape[0], Bshape[0], (A.shape[-1] + 1) // 2
+    is_on_gpu([B, A, out, absmax, state.code])
+    if B.dtype not in [torch.uint8, torch.bfloat16, torch.float16, torch.float32]:
+        raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
+    names = {torch.float16: "fp16", torch.bfloat16: "bf16", torch.float32: "fp32"}
+    if A.dtype not in names:
+        raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
+    fn = getattr(lib, f"cgemm_4bit_inference_naive_{names[A.dtype]}")
+    fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A), get_ptr(B), get_ptr(absmax), get_ptr(state.code),
+       get_ptr(out), ct.c_int32(lda), ct.c_int32(ldb), ct.c_int32(ldc), ct.c_int32(state.blocksize))
+    post_call(prev_device)
+    return out
+
+
+def gemm_4bit_supported(A: Tensor, state: QuantState) -> bool:
+    return (A.dtype in (torch.bfloat16, torch.float16) and A.is_cuda and state.shape[1] % 64 == 0
+            and A.shape[-1] == state.shape[1] and state.blocksize >= 64)
+
+
+def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = None,
+              absmax: Optional[Tensor] = None) -> Tensor:
+    """Fused 4-bit weight GEMM for any number of activation rows (the M>1 slot of
+    cgemm_4bit_inference, ref:pythonInterface.cpp:377).  out[..., n] = A[..., :] @ W^T with W the
+    dequantised [N, K] weight; replaces dequantize_4bit + F.linear (autograd/_functions.py:507).
+    B is the packed uint8 weight (any view of the N*K/2 bytes)."""
+    if not gemm_4bit_supported(A, state):
+        raise ValueError("gemm_4bit: needs bf16/fp16 activations and in_features % 64 == 0")
+    N, K = state.shape[0], state.shape[1]
+    A2 = A.reshape(-1, K)
+    if not A2.is_contiguous() or A2.data_ptr() % 16:
+        A2 = A2.contiguous()
+    rows = A2.shape[0]
+    if absmax is None:
+        absmax = _absmax_fp32(state)
+    if out is None:
+        out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
+    Bc = B if B.is_contiguous() else B.contiguous()
+    prev_device = pre_call(A.device)
+    is_on_gpu([A2, Bc, absmax, out, state.code])
+    fn = lib.cgemm_4bit_inference_code_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_4bit_inference_code_fp16
+    fn(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K), get_ptr(A2), get_ptr(Bc), get_ptr(absmax),
+       get_ptr(state.code), get_ptr(out), ct.c_int32(K), ct.c_int32((K + 1) // 2), ct.c_int32(N),
+       ct.c_int32(state.blocksize))
+    post_call(prev_device)
+    return out.view(*A.shape[:-1], N)
+
+
+# ----------------------------------------------------------------------------- LLM.int8
+def get_transform_buffer(shape, dtype, device, to_order, from_order="row", transpose=False):
+    """ref:functional.py:482-518"""
+    init_func = torch.zeros
+    dims = len(shape)
+    if dims == 2:
+        rows = shape[0]
+    elif dims == 3:
+        rows = shape[0] * shape[1]
+    cols = shape[-1]
+    state = (shape, to_order)
+    if transpose:
+        rows, cols = cols, rows
+        state = (shape[::-1], to_order)
+    if to_order == "row" or to_order == "col":
+        return init_func(shape, dtype=dtype, device=device), state
+    elif to_order == "col32":
+        cols = 32 * ((cols + 31) // 32)
+        return init_func((rows, cols), dtype=dtype, device=device), state
+    elif to_order == "col_turing":
+        cols = 32 * ((cols + 31) // 32)
+        rows = 8 * ((rows + 7) // 8)
+        return init_func((rows, cols), dtype=dtype, device=device), state
+    elif to_order == "col_ampere":
+        cols = 32 * ((cols + 31) // 32)
+        rows = 32 * ((rows + 31) // 32)
+        return init_func((rows, cols), dtype=dtype, device=device), state
+    raise NotImplementedError(f"To_order not supported: {to_order}")
+
+
+def transform(A, to_order, from_order="row", out=None, transpose=False, state=None, ld=None):
+    """Row-major int8 <-> col32 / col_turing / col_ampere tiles (ref:functional.py:2607-2653)."""
+    prev_device = pre_call(A.device)
+    if state is None:
+        state = (A.shape, from_order)
+    else:
+        from_order = state[1]
+    if out is None:
+        if to_order == "row":
+            out, new_state = torch.empty(state[0], dtype=A.dtype, device=A.device), (state[0], "row")
+        else:
+            out, new_state = get_transform_buffer(state[0], A.dtype, A.device, to_order, state[1], transpose)
+    else:
+        new_state = (state[0], to_order)
+    shape = state[0]
+    if len(shape) == 2:
+        dim1, dim2 = ct.c_int32(shape[0]), ct.c_int32(shape[1])
+    else:
+        dim1, dim2 = ct.c_int32(shape[0] * shape[1]), ct.c_int32(shape[2])
+    is_on_gpu([A, out])
+    if to_order == "col32":
+        (lib.ctransform_row2col32T if transpose else lib.ctransform_row2col32)(get_ptr(A), get_ptr(out), dim1, dim2)
+    elif to_order == "col_turing":
+        (lib.ctransform_row2turingT if transpose else lib.ctransform_row2turing)(get_ptr(A), get_ptr(out), dim1, dim2)
+    elif to_order == "col_ampere":
+        (lib.ctransform_row2ampereT if transpose else lib.ctransform_row2ampere)(get_ptr(A), get_ptr(out), dim1, dim2)
+    elif to_order == "row":
+        if from_order == "col_turing":
+            lib.ctransform_turing2row(get_ptr(A), get_ptr(out), dim1, dim2)
+        elif from_order == "col_ampere":
+            lib.ctransform_ampere2row(get_ptr(A), get_ptr(out), dim1, dim2)
+        elif from_order == "col32":
+            lib.ctransform_col322row(get_ptr(A), get_ptr(out), dim1, dim2)
+        else:
+            raise NotImplementedError(f"Transform function not implemented: From {from_order} to {to_order}")
+    else:
+        raise NotImplementedError(f"Transform function not implemented: From {from_order} to {to_order}")
+    post_call(prev_device)
+    return out, new_state
+
+
+def igemmlt(A, B, SA, SB, out=None, Sout=None, dtype=torch.int32):
+    """C = A @ B^T on int8 tiles, int32 (or int8) col32 output (ref:functional.py:2260-2352)."""
+    shapeA, shapeB = SA[0], SB[0]
+    dimsA, dimsB = len(shapeA), len(shapeB)
+    assert dimsB == 2, "Only two dimensional matrices are supported for argument B"
+    if dimsA == 2:
+        m = shapeA[0]
+    elif dimsA == 3:
+        m = shapeA[0] * shapeA[1]
+    rows = n = shapeB[0]
+    assert prod(list(shapeA)) > 0, f"Input tensor dimensions need to be > 0: {shapeA}"
+    if shapeA[0] == 0 and dimsA == 2:
+        return torch.empty((0, shapeB[0]), device=A.device, dtype=torch.float16)
+    elif shapeA[1] == 0 and dimsA == 3:
+        return torch.empty(tuple(shapeA[:2] + [shapeB[0]]), device=A.device, dtype=torch.float16)
+    if dimsA == 2 and out is None:
+        out, Sout = get_transform_buffer((shapeA[0], shapeB[0]), dtype, A.device, "col32", "row")
+    elif dimsA == 3 and out is None:
+        out, Sout = get_transform_buffer((shapeA[0], shapeA[1], shapeB[0]), dtype, A.device, "col32", "row")
+    assert dimsB != 3, "len(B.shape)==3 not supported"
+    assert A.device.type == "cuda" and B.device.type == "cuda"
+    assert A.dtype == torch.int8 and B.dtype == torch.int8
+    assert out.dtype == dtype
+    assert SA[1] == "col32"
+    assert SB[1] in ["col_turing", "col_ampere"]
+    assert Sout[1] == "col32"
+    assert shapeA[-1] == shapeB[-1], (
+        f"Matmullt only supports A @ B^T. Inner matrix dimensions do not match: A @ B = {shapeA} @ {shapeB}")
+    formatB = SB[1]
+    prev_device = pre_call(A.device)
+    k = shapeA[-1]
+    lda = ct.c_int32(m * 32)
+    if formatB == "col_turing":
+        ldb = ct.c_int32(((rows + 7) // 8) * 8 * 32)
+    else:
+        ldb = ct.c_int32(((rows + 31) // 32) * 32 * 32)
+    ldc = ct.c_int32(m * 32)
+    is_on_gpu([A, B, out])
+    fmt = "turing" if formatB == "col_turing" else "ampere"
+    fn = getattr(lib, f"cigemmlt_{fmt}_32" if dtype == torch.int32 else f"cigemmlt_{fmt}_8")
+    has_error = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A), get_ptr(B), get_ptr(out), get_ptr(None),
+                   lda, ldb, ldc)
+    if has_error == 1:
+        has_error = 100
+    if has_error == 100:
+        raise NotImplementedError("igemmlt not available (probably built with NO_CUBLASLT)")
+    if has_error:
+        raise Exception("igemmlt ran into an error!")
+    post_call(prev_device)
+    return out, Sout
+
+
+def mm_dequant(A, quant_state, row_stats, col_stats, out=None, new_row_stats=None, new_col_stats=None, bias=None):
+    """int32 col32 -> fp16 row-major with row/col stats and bias (ref:functional.py:2355-2397)."""
+    assert A.dtype == torch.int32
+    if bias is not None:
+        assert bias.dtype == torch.float16
+    out_shape = quant_state[0]
+    if len(out_shape) == 3:
+        out_shape = (out_shape[0] * out_shape[1], out_shape[2])
+    if out is None:
+        out = torch.empty(out_shape, dtype=torch.float16, device=A.device)
+    if new_row_stats is None:
+        new_row_stats = torch.empty(out_shape[0], dtype=torch.float32, device=A.device)
+    if new_col_stats is None:
+        new_col_stats = torch.empty(out_shape[1], dtype=torch.float32, device=A.device)
+    assert new_row_stats.shape[0] == row_stats.shape[0], f"{new_row_stats.shape} vs {row_stats.shape}"
+    assert new_col_stats.shape[0] == col_stats.shape[0], f"{new_col_stats.shape} vs {col_stats.shape}"
+    prev_device = pre_call(A.device)
+    is_on_gpu([A, row_stats, col_stats, out, new_row_stats, new_col_stats, bias])
+    lib.cdequant_mm_int32_fp16(get_ptr(A), get_ptr(row_stats), get_ptr(col_stats), get_ptr(out),
+                               get_ptr(new_row_stats), get_ptr(new_col_stats), get_ptr(bias),
+                               ct.c_int32(out_shape[0]), ct.c_int32(out_shape[1]))
+    post_call(prev_device)
+    return out
+
+
+def igemmlt_dequant(CA: Tensor, CB: Tensor, row_stats: Tensor, col_stats: Tensor, bias: Optional[Tensor] = None,
+                    out: Optional[Tensor] = None) -> Tensor:
+    """Fused LLM.int8 matmul on row-major int8 operands: mm_dequant(igemmlt(CA, CB)) in one launch
+    (additive entry point cigemmlt_row_dequant_fp16).  CA [m, k] int8, CB [n, k] int8 -> fp16 [m, n]."""
+    assert CA.dtype == torch.int8 and CB.dtype == torch.int8
+    m, k = CA.reshape(-1, CA.shape[-1]).shape
+    n = CB.shape[0]
+    assert CB.shape[1] == k
+    if bias is not None:
+        assert bias.dtype == torch.float16
+    CA2 = CA.reshape(m, k).contiguous()
+    CBc = CB.contiguous()
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float16, device=CA.device)
+    prev_device = pre_call(CA.device)
+    is_on_gpu([CA2, CBc, row_stats, col_stats, out, bias])
+    err = lib.cigemmlt_row_dequant_fp16(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(CA2), get_ptr(CBc),
+                                        get_ptr(out), get_ptr(row_stats), get_ptr(col_stats), get_ptr(bias),
+                                        ct.c_int32(k), ct.c_int32(k), ct.c_int32(n))
+    if err:
+        raise Exception("igemmlt ran into an error!")
+    post_call(prev_device)
+    return out
+
+
+def igemm_rowmajor(A: Tensor, B: Tensor, out: Optional[Tensor] = None) -> Tensor:
+    """Exact int8 x int8 -> int32, C = A @ B^T on row-major operands (additive cigemm_row_i32)."""
+    m, k = A.shape
+    n = B.shape[0]
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.int32, device=A.device)
+    prev_device = pre_call(A.device)
+    is_on_gpu([A, B, out])
+    err = lib.cigemm_row_i32(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A.contiguous()),
+                             get_ptr(B.contiguous()), get_ptr(out), ct.c_int32(k), ct.c_int32(k), ct.c_int32(n))
+    if err:
+        raise Exception("igemm ran into an error!")
+    post_call(prev_device)
+    return out
+
+
+def get_colrow_absmax(A, row_stats=None, col_stats=None, nnz_block_ptr=None, threshold=0.0):
+    """Row and column absmax of an fp16 matrix (ref:functional.py:2400-2435)."""
+    assert A.dtype == torch.float16
+    device = A.device
+    cols = A.shape[-1]
+    rows = A.shape[0] * A.shape[1] if len(A.shape) == 3 else A.shape[0]
+    col_tiles = (cols + 255) // 256
+    tiled_rows = ((rows + 15) // 16) * 16
+    if row_stats is None:
+        row_stats = torch.empty((rows,), dtype=torch.float32, device=device).fill_(-50000.0)
+    if col_stats is None:
+        col_stats = torch.empty((cols,), dtype=torch.float32, device=device).fill_(-50000.0)
+    if nnz_block_ptr is None and threshold > 0.0:
+        nnz_block_ptr = torch.zeros(((tiled_rows * col_tiles) + 1,), dtype=torch.int32, device=device)
+    prev_device = pre_call(A.device)
+    is_on_gpu([A, row_stats, col_stats, nnz_block_ptr])
+    lib.cget_col_row_stats(get_ptr(A), get_ptr(row_stats), get_ptr(col_stats), get_ptr(nnz_block_ptr),
+                           ct.c_float(threshold), ct.c_int32(rows), ct.c_int32(cols))
+    post_call(prev_device)
+    if threshold > 0.0:
+        nnz_block_ptr.cumsum_(0)
+    return row_stats, col_stats, nnz_block_ptr
+
+
+class COOSparseTensor:
+    def __init__(self, rows, cols, nnz, rowidx, colidx, values):
+        assert rowidx.dtype == torch.int32 and colidx.dtype == torch.int32 and values.dtype == torch.float16
+        assert values.numel() == nnz and rowidx.numel() == nnz and colidx.numel() == nnz
+        self.rows, self.cols, self.nnz = rows, cols, nnz
+        self.rowidx, self.colidx, self.values = rowidx, colidx, values
+
+
+def coo_zeros(rows, cols, nnz, device, dtype=torch.half):
+    rowidx = torch.zeros((nnz,), dtype=torch.int32, device=device)
+    colidx = torch.zeros((nnz,), dtype=torch.int32, device=device)
+    values = torch.zeros((nnz,), dtype=dtype, device=device)
+    return COOSparseTensor(rows, cols, nnz, rowidx, colidx, values)
+
+
+def double_quant(A, col_stats=None, row_stats=None, out_col=None, out_row=None, threshold=0.0):
+    """Row- and column-normalised int8 quantisation (ref:functional.py:2517-2604).
+    Returns (out_row, out_col, row_stats, col_stats, coo_tensor)."""
+    device = A.device
+    assert A.dtype == torch.half
+    assert device.type == "cuda"
+    cols = A.shape[-1]
+    rows = A.shape[0] * A.shape[1] if len(A.shape) == 3 else A.shape[0]
+    nnz_row_ptr = None
+    if row_stats is None or col_stats is None:
+        row_stats, col_stats, nnz_row_ptr = get_colrow_absmax(A, threshold=threshold)
+    if out_col is None:
+        out_col = torch.zeros(A.shape, device=device, dtype=torch.int8)
+    if out_row is None:
+        out_row = torch.zeros(A.shape, device=device, dtype=torch.int8)
+    coo_tensor = None
+    prev_device = pre_call(A.device)
+    is_on_gpu([A, col_stats, row_stats, out_col, out_row])
+    if threshold > 0.0 and nnz_row_ptr is not None and nnz_row_ptr[-1].item() > 0:
+        nnz = nnz_row_ptr[-1].item()
+        coo_tensor = coo_zeros(A.shape[0], A.shape[1], nnz, device)
+        lib.cdouble_rowcol_quant(get_ptr(A), get_ptr(row_stats), get_ptr(col_stats), get_ptr(out_col),
+                                 get_ptr(out_row), get_ptr(coo_tensor.rowidx), get_ptr(coo_tensor.colidx),
+                                 get_ptr(coo_tensor.values), get_ptr(nnz_row_ptr), ct.c_float(threshold),
+                                 ct.c_int32(rows), ct.c_int32(cols))
+        val, idx = torch.sort(coo_tensor.rowidx)
+        coo_tensor.rowidx = val
+        coo_tensor.colidx = coo_tensor.colidx[idx]
+        coo_tensor.values = coo_tensor.values[idx]
+    else:
+        lib.cdouble_rowcol_quant(get_ptr(A), get_ptr(row_stats), get_ptr(col_stats), get_ptr(out_col),
+                                 get_ptr(out_row), None, None, None, None, ct.c_float(0.0), ct.c_int32(rows),
+                                 ct.c_int32(cols))
+    post_call(prev_device)
+    return out_row, out_col, row_stats, col_stats, coo_tensor
+
+
+def extract_outliers(A, SA, idx):
+    """Gather int8 columns `idx` of a turing/ampere-tiled matrix (ref:functional.py:2914-2936)."""
+    shapeA, formatA = SA[0], SA[1]
+    assert formatA in ["col_turing", "col_ampere"]
+    assert A.device.type == "cuda"
+    out = torch.zeros((shapeA[0], idx.numel()), dtype=torch.int8, device=A.device)
+    prev_device = pre_call(A.device)
+    fn = lib.cextractOutliers_turing if formatA == "col_turing" else lib.cextractOutliers_ampere
+    fn(get_ptr(A), get_ptr(idx), get_ptr(out), ct.c_int32(idx.numel()), ct.c_int32(shapeA[0]),
+       ct.c_int32(shapeA[1]))
+    post_call(prev_device)
+    return out

@@ -1,0 +1,139 @@
+/* C-ABI of libbitsandbytes_hip.so — the drop-in boundary for the quantized-matmul hot path.
+ *
+ * Every entry point below keeps the name, argument order, types and meaning of the reference's
+ * exported symbol (abhilash1910/bitsandbytes-SYCL, ref:sycl/pythonInterface.cpp, cited per line),
+ * so the reference's ctypes layer (ref:python_src_quants/functional.py) can bind it unchanged.
+ * Device pointers are HIP device pointers on the current device; launches go to the stream set
+ * by cset_stream (default: the null stream).  Launches are asynchronous.
+ *
+ * Types: fp16 = IEEE binary16 (passed as `unsigned short` bit patterns here, `sycl::half` in the
+ * reference); bf16 = bfloat16 (`unsigned short` bits, `sycl::ext::oneapi::bfloat16` in the reference).
+ * Symbols marked [additive] are not in the reference ABI and never change the meaning of one that is.
+ */
+#ifndef BNB_HIP_H
+#define BNB_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef unsigned short bnb_fp16;
+typedef unsigned short bnb_bf16;
+
+/* ---- context / loader probes: ref:sycl/pythonInterface.cpp:295-296, 380-398 ---- */
+void* get_context(void);                                   /* pythonInterface.cpp:295 */
+void* get_cusparse(void);                                  /* pythonInterface.cpp:296 */
+void* cget_managed_ptr(size_t bytes);                      /* pythonInterface.cpp:380 */
+void cprefetch(void* ptr, size_t bytes, int device);       /* pythonInterface.cpp:389 */
+
+/* ---- blockwise quantize: ref:sycl/pythonInterface.cpp:203-217 ----
+ * absmax[b] = max|A| over block b (fp32); code = NULL for fp4/nf4, the 256-entry map for 8-bit.
+ * out: ceil(n/2) bytes for fp4/nf4 (high nibble = even element), n bytes for 8-bit. */
+void cquantize_blockwise_fp16(float* code, bnb_fp16* A, float* absmax, unsigned char* out, int blocksize, const int n);     /* :203 */
+void cquantize_blockwise_fp16_fp4(float* code, bnb_fp16* A, float* absmax, unsigned char* out, int blocksize, const int n); /* :204 */
+void cquantize_blockwise_fp16_nf4(float* code, bnb_fp16* A, float* absmax, unsigned char* out, int blocksize, const int n); /* :205 */
+void cquantize_blockwise_fp32(float* code, float* A, float* absmax, unsigned char* out, int blocksize, const int n);        /* :207 */
+void cquantize_blockwise_fp32_fp4(float* code, float* A, float* absmax, unsigned char* out, int blocksize, const int n);    /* :208 */
+void cquantize_blockwise_fp32_nf4(float* code, float* A, float* absmax, unsigned char* out, int blocksize, const int n);    /* :209 */
+void cquantize_blockwise_bf16(float* code, bnb_bf16* A, float* absmax, unsigned char* out, int blocksize, const int n);     /* :215 */
+void cquantize_blockwise_bf16_fp4(float* code, bnb_bf16* A, float* absmax, unsigned char* out, int blocksize, const int n); /* :216 */
+void cquantize_blockwise_bf16_nf4(float* code, bnb_bf16* A, float* absmax, unsigned char* out, int blocksize, const int n); /* :217 */
+
+/* ---- blockwise dequantize: ref:sycl/pythonInterface.cpp:199-221 ---- out[i] = T(code[q_i] * absmax[i/bs]) */
+void cdequantize_blockwise_fp16_fp4(float* code, unsigned char* A, float* absmax, bnb_fp16* out, int blocksize, const int n); /* :199 */
+void cdequantize_blockwise_fp16(float* code, unsigned char* A, float* absmax, bnb_fp16* out, int blocksize, const int n);     /* :200 */
+void cdequantize_blockwise_fp16_nf4(float* code, unsigned char* A, float* absmax, bnb_fp16* out, int blocksize, const int n); /* :201 */
+void cdequantize_blockwise_fp32(float* code, unsigned char* A, float* absmax, float* out, int blocksize, const int n);        /* :211 */
+void cdequantize_blockwise_fp32_fp4(float* code, unsigned char* A, float* absmax, float* out, int blocksize, const int n);    /* :212 */
+void cdequantize_blockwise_fp32_nf4(float* code, unsigned char* A, float* absmax, float* out, int blocksize, const int n);    /* :213 */
+void cdequantize_blockwise_bf16(float* code, unsigned char* A, float* absmax, bnb_bf16* out, int blocksize, const int n);     /* :219 */
+void cdequantize_blockwise_bf16_fp4(float* code, unsigned char* A, float* absmax, bnb_bf16* out, int blocksize, const int n); /* :220 */
+void cdequantize_blockwise_bf16_nf4(float* code, unsigned char* A, float* absmax, bnb_bf16* out, int blocksize, const int n); /* :221 */
+
+/* ---- host-pointer CPU-path entry points: ref:sycl/pythonInterface.cpp:419-420 (cpu_ops.cpp semantics:
+ * division A/absmax, nearest code with ties to the left, code[0] := -1 in place).  Executed on the GPU
+ * (host buffers staged through HBM), synchronous on return. */
+void cquantize_blockwise_cpu_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize, long long n);   /* :419 */
+void cdequantize_blockwise_cpu_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize, long long n); /* :420 */
+/* [additive] device-pointer form of the CPU-path dequantize (one byte per element, any blocksize) */
+void cdequantize_blockwise_bytes_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize, long long n);
+
+/* ---- 4-bit GEMV (M == 1): ref:sycl/pythonInterface.cpp:408-415 ----
+ * out[r] = sum_k A[k] * datatype[q(r,k)] * absmax[(2*ldb*r + k)/blocksize]; m = out_features, k = in_features */
+void cgemm_4bit_inference_naive_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, float* absmax, float* datatype,
+                                     bnb_fp16* out, int lda, int ldb, int ldc, int blocksize);   /* :408 */
+void cgemm_4bit_inference_naive_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, float* absmax, float* datatype,
+                                     bnb_bf16* out, int lda, int ldb, int ldc, int blocksize);   /* :411 */
+void cgemm_4bit_inference_naive_fp32(int m, int n, int k, float* A, unsigned char* B, float* absmax, float* datatype,
+                                     float* out, int lda, int ldb, int ldc, int blocksize);      /* :414 */
+
+/* ---- 4-bit GEMM (any number of activation rows): ref:sycl/pythonInterface.cpp:377-378 (slot of the
+ * broken kgemm_4bit_inference, re-implemented as a fused NF4 GEMM) ----
+ * m = out_features, n = activation rows, k = in_features (k % 64 == 0):
+ * out[t*ldc + r] = sum_k A[t*lda + k] * W[r, k],  W[r, k] = T(code[q(r,k)] * absmax[(2*ldb*r + k)/blocksize]) */
+void cgemm_4bit_inference(int m, int n, int k, bnb_fp16* A, unsigned char* B, float* absmax, bnb_fp16* out, int lda,
+                          int ldb, int ldc, int blocksize);                                      /* :377, NF4 table */
+/* [additive] bf16 sibling (NF4) and table-driven variants (any 16-entry code, e.g. FP4) */
+void cgemm_4bit_inference_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, float* absmax, bnb_bf16* out, int lda,
+                               int ldb, int ldc, int blocksize);
+void cgemm_4bit_inference_code_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, float* absmax, float* datatype,
+                                    bnb_fp16* out, int lda, int ldb, int ldc, int blocksize);
+void cgemm_4bit_inference_code_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, float* absmax, float* datatype,
+                                    bnb_bf16* out, int lda, int ldb, int ldc, int blocksize);
+
+/* ---- LLM.int8 statistics and quantisation: ref:sycl/pythonInterface.cpp:333-339 ---- */
+void cget_col_row_stats(bnb_fp16* A, float* rowStats, float* colStats, int* nnz_count_row, float nnz_threshold, int rows,
+                        int cols);                                                               /* :335 */
+void cdouble_rowcol_quant(bnb_fp16* A, float* rowStats, float* colStats, char* out_col_normed, char* out_row_normed,
+                          int* rowidx, int* colidx, bnb_fp16* val, int* nnz_row_ptr, float threshold, int rows,
+                          int cols);                                                             /* :338 */
+
+/* ---- tile layouts: ref:sycl/pythonInterface.cpp:341-357 (row-major int8 -> format of A, or of A^T for *T) ---- */
+void ctransform_row2col32(char* A, char* out, int rows, int cols);     /* :341 */
+void ctransform_row2col32T(char* A, char* out, int rows, int cols);    /* :344 */
+void ctransform_row2turing(char* A, char* out, int rows, int cols);    /* :347 */
+void ctransform_row2turingT(char* A, char* out, int rows, int cols);   /* :350 */
+void ctransform_row2ampere(char* A, char* out, int rows, int cols);    /* :353 */
+void ctransform_row2ampereT(char* A, char* out, int rows, int cols);   /* :356 */
+/* [additive] inverse transforms; functional.py:2645-2647 calls the first two (never exported by the reference, Q18) */
+void ctransform_turing2row(char* A, char* out, int rows, int cols);
+void ctransform_ampere2row(char* A, char* out, int rows, int cols);
+void ctransform_col322row(char* A, char* out, int rows, int cols);
+
+/* ---- int8 GEMM C = A @ B^T (A col32 m x k, B col_turing/col_ampere n x k, C col32): ref:sycl/pythonInterface.cpp:298-316.
+ * Returns 0 on success, 1 on error (Python maps 1 -> NotImplementedError, functional.py:2341-2348). No context argument. */
+int cigemmlt_turing_32(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc);          /* :298 */
+int cigemmlt_turing_8(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc);           /* :303 */
+int cigemmlt_turing_8_rowscale(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc);  /* :306 */
+int cigemmlt_ampere_32(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc);          /* :309 */
+int cigemmlt_ampere_8_rowscale(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc);  /* :312 */
+int cigemmlt_ampere_8(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc);           /* :315 */
+/* [additive] row-major operands: fused igemmlt + dequant_mm_int32_fp16 (fp16 [m, n] out), and exact int32 */
+int cigemmlt_row_dequant_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, bnb_fp16* out, const float* rowStats,
+                              const float* colStats, const bnb_fp16* bias, int lda, int ldb, int ldc);
+int cigemm_row_i32(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc);
+
+/* ---- int32 -> fp16 dequant: ref:sycl/pythonInterface.cpp:333 ----
+ * out[r, c] = half(((float(C[r,c]) * 6.200012e-05f) * rowStats[r]) * colStats[c] + bias[c]), C in col32 */
+void cdequant_mm_int32_fp16(int* A, float* rowStats, float* colStats, bnb_fp16* out, float* newRowStats, float* newcolStats,
+                            bnb_fp16* bias, int numRows, int numCols);                           /* :333 */
+
+/* ---- outlier column gather: ref:sycl/pythonInterface.cpp:368-369 ---- */
+void cextractOutliers_turing(char* A, int* idx, char* out, int idx_size, int rows, int cols);   /* :368 */
+void cextractOutliers_ampere(char* A, int* idx, char* out, int idx_size, int rows, int cols);   /* :369 */
+
+/* ---- [additive] runtime ---- */
+void cset_stream(void* stream);            /* hipStream_t used by every launch (NULL = null stream) */
+void* cget_stream(void);
+int cget_last_error(void);                 /* returns and clears the last error code (0 = none) */
+const char* cget_last_error_message(void);
+int cget_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BNB_HIP_H */

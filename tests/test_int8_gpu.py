@@ -1,0 +1,175 @@
+"""GPU parity: LLM.int8 path — stats, double_quant, layouts, igemmlt, mm_dequant (bit-exact),
+and the fused row-major igemmlt+dequant kernel."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import same_bits
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _F():
+    import python_src_quants.functional as F
+    return F
+
+
+def test_double_quant_golden(golden, dev):
+    F = _F()
+    A = torch.from_numpy(golden["dq_A"]).to(dev)
+    orow, ocol, rs, cs, coo = F.double_quant(A)
+    assert coo is None
+    assert same_bits(rs.cpu().numpy(), golden["dq_rs"])
+    assert same_bits(cs.cpu().numpy(), golden["dq_cs"])
+    assert same_bits(orow.cpu().numpy(), golden["dq_row"])
+    assert same_bits(ocol.cpu().numpy(), golden["dq_col"])
+
+
+@pytest.mark.parametrize("shape", [(4096, 4096), (1, 7), (17, 300), (513, 1030), (2048, 11008)])
+def test_double_quant_random(dev, shape):
+    F = _F()
+    torch.manual_seed(shape[0])
+    A = (torch.randn(*shape, device=dev) * 4).half()
+    A[0, : min(5, shape[1])] = 0
+    orow, ocol, rs, cs, _ = F.double_quant(A)
+    An = A.cpu().numpy()
+    ers, ecs, _ = ref.colrow_absmax(An)
+    assert same_bits(rs.cpu().numpy(), ers) and same_bits(cs.cpu().numpy(), ecs)
+    er, ec = ref.double_quant(An, ers, ecs)
+    assert same_bits(orow.cpu().numpy(), er) and same_bits(ocol.cpu().numpy(), ec)
+
+
+def test_colrow_stats_threshold(dev):
+    F = _F()
+    torch.manual_seed(0)
+    A = torch.randn(100, 600, device=dev).half()
+    A[3, 10] = 20
+    A[50, 599] = -30
+    A[99, 0] = 7
+    rs, cs, nnz = F.get_colrow_absmax(A, threshold=6.0)
+    ers, ecs, enr = ref.colrow_absmax(A.cpu().numpy(), threshold=6.0)
+    assert same_bits(rs.cpu().numpy(), ers) and same_bits(cs.cpu().numpy(), ecs)
+    assert nnz[-1].item() == int(enr.sum()) == 3
+    orow, ocol, rs2, cs2, coo = F.double_quant(A, threshold=6.0)
+    assert coo is not None and coo.nnz == 3
+    got = sorted(zip(coo.rowidx.tolist(), coo.colidx.tolist(), coo.values.float().tolist()))
+    assert got == [(3, 10, 20.0), (50, 599, -30.0), (99, 0, 7.0)]
+    assert orow[3, 10].item() == 0 and orow[50, 599].item() == 0
+
+
+@pytest.mark.parametrize("fmt", ["col32", "col_turing", "col_ampere"])
+@pytest.mark.parametrize("shape", [(64, 96), (33, 70), (4096, 4096), (1, 1), (130, 4000)])
+def test_transforms(dev, fmt, shape):
+    F = _F()
+    rng = np.random.default_rng(shape[1])
+    A = rng.integers(-128, 128, size=shape, dtype=np.int8)
+    At = torch.from_numpy(A).to(dev)
+    for transpose in (False, True):
+        out, st = F.transform(At, fmt, transpose=transpose)
+        assert same_bits(out.cpu().numpy(), ref.transform(A, fmt, transpose=transpose)), (fmt, transpose)
+    if fmt != "col32":
+        out, st = F.transform(At, fmt)
+        back, _ = F.transform(out, "row", state=st)
+        assert torch.equal(back, At)
+
+
+def test_transforms_golden(golden, dev):
+    F = _F()
+    A = torch.from_numpy(golden["ig_A"]).to(dev)
+    for fmt in ("col32", "col_turing", "col_ampere"):
+        assert same_bits(F.transform(A, fmt)[0].cpu().numpy(), golden[f"tf_{fmt}"])
+        assert same_bits(F.transform(A, fmt, transpose=True)[0].cpu().numpy(), golden[f"tfT_{fmt}"])
+
+
+@pytest.mark.parametrize("formatB", ["col_turing", "col_ampere"])
+@pytest.mark.parametrize("mnk", [(64, 40, 96), (4096, 4096, 4096), (1, 1, 1), (77, 300, 1000), (256, 129, 128)])
+def test_igemmlt_exact(dev, formatB, mnk):
+    F = _F()
+    m, n, k = mnk
+    rng = np.random.default_rng(m + n + k)
+    A = rng.integers(-127, 128, size=(m, k), dtype=np.int8)
+    B = rng.integers(-127, 128, size=(n, k), dtype=np.int8)
+    At, Bt = torch.from_numpy(A).to(dev), torch.from_numpy(B).to(dev)
+    C32A, SA = F.transform(At, "col32")
+    CxB, SB = F.transform(Bt, formatB)
+    out32, Sout = F.igemmlt(C32A, CxB, SA, SB)
+    got = ref.untransform(out32.cpu().numpy(), m, n, "col32")
+    if m * n * k <= 2e8:
+        exp = ref.igemmlt(A, B)
+    else:
+        exp = (torch.from_numpy(A).to(dev).double() @ torch.from_numpy(B).to(dev).double().T).cpu().numpy()
+        exp = exp.astype(np.int64).astype(np.int32)
+    assert np.array_equal(got, exp)
+
+
+def test_igemmlt_golden_and_mm_dequant(golden, dev):
+    F = _F()
+    A = torch.from_numpy(golden["ig_A"]).to(dev)
+    B = torch.from_numpy(golden["ig_B"]).to(dev)
+    C32A, SA = F.transform(A, "col32")
+    CxB, SB = F.transform(B, "col_turing")
+    out32, Sout = F.igemmlt(C32A, CxB, SA, SB)
+    m, n = golden["ig_C"].shape
+    assert np.array_equal(ref.untransform(out32.cpu().numpy(), m, n, "col32"), golden["ig_C"])
+    rs = torch.from_numpy(golden["ig_rstat"]).to(dev)
+    cs = torch.from_numpy(golden["ig_cstat"]).to(dev)
+    bias = torch.from_numpy(golden["ig_bias"]).to(dev)
+    D = F.mm_dequant(out32, Sout, rs, cs, bias=bias)
+    assert same_bits(D.cpu().numpy(), golden["ig_D"])
+
+
+def test_igemmlt_int8_out(dev):
+    F = _F()
+    rng = np.random.default_rng(9)
+    m, n, k = 70, 50, 64
+    A = rng.integers(-4, 5, size=(m, k), dtype=np.int8)
+    B = rng.integers(-4, 5, size=(n, k), dtype=np.int8)
+    At, Bt = torch.from_numpy(A).to(dev), torch.from_numpy(B).to(dev)
+    C32A, SA = F.transform(At, "col32")
+    CxB, SB = F.transform(Bt, "col_ampere")
+    out8, Sout = F.igemmlt(C32A, CxB, SA, SB, dtype=torch.int8)
+    got = ref.untransform(out8.cpu().numpy(), m, n, "col32")
+    assert np.array_equal(got, ref.igemmlt_int8_out(A, B))
+    # row-scaled variant through the raw ABI
+    scale = torch.from_numpy(rng.uniform(0.01, 0.2, m).astype(np.float32)).to(dev)
+    out = torch.zeros_like(out8)
+    F.lib.cigemmlt_ampere_8_rowscale(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(C32A), F.get_ptr(CxB),
+                                     F.get_ptr(out), F.get_ptr(scale), ct.c_int32(32 * m), ct.c_int32(32 * ((n + 31) // 32) * 32),
+                                     ct.c_int32(32 * m))
+    torch.cuda.synchronize()
+    got = ref.untransform(out.cpu().numpy(), m, n, "col32")
+    assert np.array_equal(got, ref.igemmlt_int8_out(A, B, scale.cpu().numpy()))
+
+
+@pytest.mark.parametrize("mnk", [(4096, 4096, 4096), (300, 200, 448), (1, 64, 128), (129, 257, 1000)])
+def test_igemmlt_row_dequant_fused(dev, mnk):
+    F = _F()
+    m, n, k = mnk
+    rng = np.random.default_rng(k)
+    A = rng.integers(-127, 128, size=(m, k), dtype=np.int8)
+    B = rng.integers(-127, 128, size=(n, k), dtype=np.int8)
+    rs = rng.uniform(0.5, 2, m).astype(np.float32)
+    cs = rng.uniform(0.5, 2, n).astype(np.float32)
+    bias = rng.standard_normal(n).astype(np.float16)
+    At, Bt = torch.from_numpy(A).to(dev), torch.from_numpy(B).to(dev)
+    out = F.igemmlt_dequant(At, Bt, torch.from_numpy(rs).to(dev), torch.from_numpy(cs).to(dev),
+                            bias=torch.from_numpy(bias).to(dev))
+    C = F.igemm_rowmajor(At, Bt)
+    if m * n * k <= 2e8:
+        assert np.array_equal(C.cpu().numpy(), ref.igemmlt(A, B))
+    exp = ref.mm_dequant(C.cpu().numpy(), rs, cs, bias)
+    assert same_bits(out.cpu().numpy(), exp)
+
+
+def test_extract_outliers(dev):
+    F = _F()
+    rng = np.random.default_rng(4)
+    B = rng.integers(-127, 128, size=(40, 96), dtype=np.int8)
+    idx = torch.tensor([0, 5, 31, 32, 95], dtype=torch.int32, device=dev)
+    for fmt in ("col_turing", "col_ampere"):
+        CxB, SB = F.transform(torch.from_numpy(B).to(dev), fmt)
+        out = F.extract_outliers(CxB, SB, idx)
+        assert np.array_equal(out.cpu().numpy(), B[:, idx.cpu().numpy()])

@@ -1,0 +1,141 @@
+"""GPU parity: 4-bit GEMV (decode) and the fused 4-bit GEMM (prefill) vs the CPU oracle.
+
+Floating point, so parity is a tolerance: rtol = 2e-2 and
+atol = 2e-2 * rms(out) for bf16 outputs (fp16: 1e-2), against an fp64 restatement; plus the
+reference test's own bound mean|out - out_fp| < 0.115 (tests_pvc/autograd.py:388-391).
+"""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import to_numpy, to_torch
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _F():
+    import python_src_quants.functional as F
+    return F
+
+
+def _close(got, exp, rtol, arel):
+    got = np.asarray(got, np.float64)
+    exp = np.asarray(exp, np.float64)
+    atol = arel * np.sqrt(np.mean(exp**2)) + 1e-30
+    bad = np.abs(got - exp) > atol + rtol * np.abs(exp)
+    return bad.mean(), np.abs(got - exp).max()
+
+
+def test_gemv_golden(golden, dev):
+    F = _F()
+    N, K, bs = golden["gemv_meta"].tolist()
+    x = to_torch(golden["gemv_x"], "bf16", dev)
+    q = torch.from_numpy(golden["gemv_q"]).to(dev)
+    absmax = torch.from_numpy(golden["gemv_absmax"]).to(dev)
+    code = torch.from_numpy(ref.nf4_table()).to(dev)
+    out = torch.empty(N, dtype=torch.bfloat16, device=dev)
+    F.lib.cgemm_4bit_inference_naive_bf16(ct.c_int32(N), ct.c_int32(1), ct.c_int32(K), F.get_ptr(x), F.get_ptr(q),
+                                          F.get_ptr(absmax), F.get_ptr(code), F.get_ptr(out), ct.c_int32(N),
+                                          ct.c_int32(K // 2), ct.c_int32(N), ct.c_int32(bs))
+    torch.cuda.synchronize()
+    frac, _ = _close(ref.bf16_bits_to_f32(to_numpy(out, "bf16")), golden["gemv_y"], 2e-2, 2e-2)
+    assert frac == 0.0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("shape", [(11008, 4096), (4096, 11008), (1000, 192), (77, 64 * 33)])
+def test_gemv_functional(dev, dtype, qt, shape):
+    F = _F()
+    N, K = shape
+    torch.manual_seed(N + K)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    for nested in (False, True):
+        q, st = F.quantize_4bit(W, blocksize=64, quant_type=qt, compress_statistics=nested)
+        x = torch.randn(1, K, device=dev, dtype=dtype)
+        y = F.gemv_4bit(x, q.t(), state=st)
+        assert y.shape == (1, N) and y.dtype == dtype
+        absmax = F._absmax_fp32(st).cpu().numpy()
+        exp = ref.gemv_4bit(x.float().cpu().numpy()[0], q.cpu().numpy(), absmax, N, K, 64, st.code.cpu().numpy())
+        tol = {torch.bfloat16: 2e-2, torch.float16: 1e-2, torch.float32: 1e-4}[dtype]
+        frac, err = _close(y.float().cpu().numpy()[0], exp, tol, tol)
+        assert frac == 0.0, (nested, err)
+
+
+def test_gemv_generic_path(dev):
+    """K not a multiple of 32 / unaligned B -> the general kernel path."""
+    F = _F()
+    N, K, bs = 50, 64 * 3 + 30, 64
+    rng = np.random.default_rng(2)
+    w = (rng.standard_normal(N * K) * 0.1).astype(np.float32)
+    absmax, q = ref.quantize_blockwise(w, bs, "nf4")      # flat blocks straddle rows: (r*K + k)/bs
+    ldb = (K + 1) // 2
+    x = rng.standard_normal(K).astype(np.float32)
+    X = torch.from_numpy(x).to(dev)
+    Q = torch.from_numpy(q).to(dev)
+    AM = torch.from_numpy(absmax).to(dev)
+    code = torch.from_numpy(ref.nf4_table()).to(dev)
+    out = torch.empty(N, device=dev)
+    F.lib.cgemm_4bit_inference_naive_fp32(ct.c_int32(N), ct.c_int32(1), ct.c_int32(K), F.get_ptr(X), F.get_ptr(Q),
+                                          F.get_ptr(AM), F.get_ptr(code), F.get_ptr(out), ct.c_int32(N),
+                                          ct.c_int32(ldb), ct.c_int32(N), ct.c_int32(bs))
+    torch.cuda.synchronize()
+    exp = ref.gemv_4bit(x, q, absmax, N, K, bs, ref.nf4_table())
+    assert np.allclose(out.cpu().numpy(), exp, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("mnk", [(1, 256, 128), (130, 300, 320), (256, 384, 1024), (64, 128, 64), (333, 1000, 576)])
+def test_gemm_4bit_vs_oracle(dev, dtype, qt, mnk):
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M * 31 + N)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type=qt)
+    Y = F.gemm_4bit(X, q, st)
+    assert Y.shape == (M, N) and Y.dtype == dtype
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), st.absmax.cpu().numpy(), N, K, 64,
+                                    st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
+    assert frac == 0.0, err
+    # the reference path for M>1 (dequantize_4bit + linear) agrees too
+    Wd = F.dequantize_4bit(q, st)
+    Yref = torch.nn.functional.linear(X.float(), Wd.float())
+    assert (Y.float() - Yref).abs().mean().item() < 0.115
+
+
+def test_gemm_4bit_legacy_abi_nf4_fp16(dev):
+    """cgemm_4bit_inference (ref ABI slot, fp16, NF4 hard-coded)."""
+    F = _F()
+    M, N, K = 96, 256, 512
+    torch.manual_seed(3)
+    W = torch.randn(N, K, device=dev, dtype=torch.float16) * 0.05
+    X = torch.randn(M, K, device=dev, dtype=torch.float16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
+    out = torch.empty(M, N, device=dev, dtype=torch.float16)
+    F.lib.cgemm_4bit_inference(ct.c_int32(N), ct.c_int32(M), ct.c_int32(K), F.get_ptr(X), F.get_ptr(q),
+                               F.get_ptr(st.absmax), F.get_ptr(out), ct.c_int32(K), ct.c_int32(K // 2), ct.c_int32(N),
+                               ct.c_int32(64))
+    torch.cuda.synchronize()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), st.absmax.cpu().numpy(), N, K, 64,
+                                    ref.nf4_table(), "fp16")
+    frac, err = _close(out.float().cpu().numpy(), exp, 1e-2, 1e-2)
+    assert frac == 0.0, err
+
+
+def test_gemm_4bit_asymmetric_identity(dev):
+    """A = I and asymmetric W: catches a transposed C write (guide §3)."""
+    F = _F()
+    K = N = 128
+    X = torch.eye(K, device=dev, dtype=torch.bfloat16)
+    W = torch.arange(N * K, device=dev, dtype=torch.float32).reshape(N, K).remainder(7).sub(3).div(3).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
+    Y = F.gemm_4bit(X, q, st)
+    Wd = F.dequantize_4bit(q, st)
+    assert torch.equal(Y, Wd.t().contiguous())

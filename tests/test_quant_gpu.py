@@ -1,0 +1,169 @@
+"""GPU parity: blockwise quantize/dequantize (HIP) vs the CPU oracle — bit-exact.
+
+Covers cquantize_blockwise_* / cdequantize_blockwise_* (ref:sycl/pythonInterface.cpp:199-221)
+for fp32/fp16/bf16 x {nf4, fp4, dynamic 8-bit} x blocksizes 64..4096, ragged tails (n not a
+multiple of the blocksize, odd n), n == 1, all-zero blocks, NaN, and misaligned pointers.
+"""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import DTYPES, same_bits, to_numpy, to_torch
+from oracle import ref
+from oracle.maps import create_dynamic_map
+
+pytestmark = pytest.mark.gpu
+
+
+def _F():
+    import python_src_quants.functional as F
+    return F
+
+
+def _quant_abi(F, dtype, qtype):
+    suffix = "" if qtype == "8bit" else f"_{qtype}"
+    return getattr(F.lib, f"cquantize_blockwise_{dtype}{suffix}"), getattr(F.lib, f"cdequantize_blockwise_{dtype}{suffix}")
+
+
+def _run_quant(F, dev, a_np, dtype, qtype, bs, code_np):
+    n = a_np.size
+    A = to_torch(a_np, dtype, dev)
+    nb = (n + bs - 1) // bs
+    absmax = torch.zeros(nb, dtype=torch.float32, device=dev)
+    out = torch.zeros(n if qtype == "8bit" else (n + 1) // 2, dtype=torch.uint8, device=dev)
+    code = torch.from_numpy(code_np).to(dev)
+    qfn, _ = _quant_abi(F, dtype, qtype)
+    qfn(F.get_ptr(code if qtype == "8bit" else None), F.get_ptr(A), F.get_ptr(absmax), F.get_ptr(out), ct.c_int32(bs), ct.c_int(n))
+    torch.cuda.synchronize()
+    assert F.lib.cget_last_error() == 0
+    return absmax.cpu().numpy(), out.cpu().numpy()
+
+
+def _run_dequant(F, dev, q_np, absmax_np, n, qtype, bs, out_dtype, code_np):
+    q = torch.from_numpy(q_np).to(dev)
+    absmax = torch.from_numpy(absmax_np).to(dev)
+    out = torch.empty(n, dtype=DTYPES[out_dtype], device=dev)
+    code = torch.from_numpy(code_np).to(dev)
+    _, dfn = _quant_abi(F, out_dtype, qtype)
+    dfn(F.get_ptr(code if qtype == "8bit" else None), F.get_ptr(q), F.get_ptr(absmax), F.get_ptr(out), ct.c_int(bs), ct.c_int(n))
+    torch.cuda.synchronize()
+    assert F.lib.cget_last_error() == 0
+    return to_numpy(out, out_dtype)
+
+
+def test_golden_quant_dequant(golden, dev):
+    F = _F()
+    code = golden["dynamic_code"]
+    for i in range(int(golden["n_quant_cases"])):
+        di, qi, bs, n = golden[f"q{i}_meta"].tolist()
+        dtype, qtype = ["fp32", "fp16", "bf16"][di], ["nf4", "fp4", "8bit"][qi]
+        absmax, q = _run_quant(F, dev, golden[f"q{i}_in"], dtype, qtype, bs, code)
+        assert same_bits(absmax, golden[f"q{i}_absmax"]), (i, dtype, qtype, bs, n, "absmax")
+        assert same_bits(q, golden[f"q{i}_q"]), (i, dtype, qtype, bs, n, "codes")
+        for od in ("fp32", "fp16", "bf16"):
+            y = _run_dequant(F, dev, golden[f"q{i}_q"], golden[f"q{i}_absmax"], n, qtype, bs, od, code)
+            assert same_bits(y, golden[f"q{i}_deq_{od}"]), (i, dtype, qtype, bs, n, od)
+
+
+@pytest.mark.parametrize("qtype", ["nf4", "fp4", "8bit"])
+@pytest.mark.parametrize("bs", [64, 128, 256, 512, 1024, 2048, 4096])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
+def test_random_sizes_bit_exact(dev, qtype, bs, dtype):
+    F = _F()
+    code = create_dynamic_map()
+    rng = np.random.default_rng(bs * 7 + len(qtype))
+    for n in (bs * 37 + 3, bs - 1, 2 * bs, 1, 131071):
+        x = (rng.standard_normal(n) * rng.uniform(0.1, 10)).astype(np.float32)
+        if n > 3:
+            x[rng.integers(0, n, 3)] = np.nan
+        a = ref.f32_to_bf16_bits(x) if dtype == "bf16" else x.astype(np.float16 if dtype == "fp16" else np.float32)
+        xf = ref.as_f32(a, dtype)
+        ea, eq = ref.quantize_blockwise(xf, bs, qtype, code=code)
+        absmax, q = _run_quant(F, dev, a, dtype, qtype, bs, code)
+        assert same_bits(absmax, ea), (n, "absmax")
+        assert same_bits(q, eq), (n, "codes", np.flatnonzero(q != eq)[:8])
+        for od in ("bf16", "fp32"):
+            y = _run_dequant(F, dev, eq, ea, n, qtype, bs, od, code)
+            assert same_bits(y, ref.dequantize_blockwise(eq, ea, bs, n, qtype, od, code=code)), (n, od)
+
+
+def test_zero_block_and_misaligned(dev):
+    F = _F()
+    n, bs = 64 * 9, 64
+    x = np.random.default_rng(0).standard_normal(n + 8).astype(np.float32)
+    x[65:129] = 0                             # = elements 64..127 of the offset view below
+    base = torch.from_numpy(x).to(dev)
+    A = base[1:n + 1]                         # 4-byte offset: forces the unaligned (scalar) path
+    a_np = x[1:n + 1]
+    for qtype in ("nf4", "fp4"):
+        absmax = torch.zeros(n // bs, device=dev)
+        outbuf = torch.zeros((n + 1) // 2 + 1, dtype=torch.uint8, device=dev)
+        out = outbuf[1:]                      # odd byte offset
+        getattr(F.lib, f"cquantize_blockwise_fp32_{qtype}")(None, F.get_ptr(A), F.get_ptr(absmax), F.get_ptr(out),
+                                                            ct.c_int32(bs), ct.c_int(n))
+        ea, eq = ref.quantize_blockwise(a_np, bs, qtype)
+        assert same_bits(absmax.cpu().numpy(), ea)
+        assert same_bits(out.cpu().numpy(), eq)
+        assert ea[1] == 0 and np.all(eq[32:64] == 0)
+
+
+def test_functional_4bit_roundtrip(dev):
+    F = _F()
+    torch.manual_seed(0)
+    for qt in ("nf4", "fp4"):
+        for dt in (torch.bfloat16, torch.float16, torch.float32):
+            w = torch.randn(512, 320, device=dev, dtype=dt)
+            q, st = F.quantize_4bit(w, blocksize=64, quant_type=qt)
+            assert q.shape == ((512 * 320 + 1) // 2, 1) and q.dtype == torch.uint8
+            wd = F.dequantize_4bit(q, st)
+            assert wd.shape == w.shape and wd.dtype == dt
+            # reference's own error bound style (functional round trip)
+            err = (wd.float() - w.float()).abs().mean().item()
+            assert err < (0.12 if qt == "nf4" else 0.15)
+            # nested statistics (compress_statistics=True, the Linear4bit default)
+            q2, st2 = F.quantize_4bit(w, blocksize=64, quant_type=qt, compress_statistics=True)
+            assert torch.equal(q2, q) and st2.nested
+            wd2 = F.dequantize_4bit(q2, st2)
+            assert (wd2.float() - wd.float()).abs().max().item() < 0.05 * w.abs().max().item()
+
+
+def test_functional_nested_matches_oracle(dev):
+    """quantize_4bit(compress_statistics=True): nested absmax bit-exact vs oracle given torch's offset."""
+    F = _F()
+    torch.manual_seed(1)
+    w = torch.randn(256, 512, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(w, blocksize=64, quant_type="nf4", compress_statistics=True)
+    xf = ref.as_f32(to_numpy(w.reshape(-1), "bf16"), "bf16")
+    absmax, eq = ref.quantize_blockwise(xf, 64, "nf4")
+    assert same_bits(q.cpu().numpy().reshape(-1), eq)
+    off = np.float32(st.offset.item())
+    ea2, eq2 = ref.quantize_blockwise((absmax - off).astype(np.float32), 256, "8bit", code=st.state2.code.cpu().numpy())
+    assert same_bits(st.absmax.cpu().numpy(), eq2)
+    assert same_bits(st.state2.absmax.cpu().numpy(), ea2)
+    full = F.dequantize_blockwise(st.absmax, st.state2) + st.offset
+    exp = ref.nested_absmax(eq2, ea2, st.state2.code.cpu().numpy(), off)
+    assert same_bits(full.cpu().numpy(), exp)
+
+
+def test_cpu_path_entry_points(golden, dev):
+    """cquantize_blockwise_cpu_fp32 / cdequantize_blockwise_cpu_fp32 (host pointers, cpu_ops.cpp semantics)."""
+    F = _F()
+    A = torch.from_numpy(golden["cpu_A"].copy())
+    code = torch.from_numpy(create_dynamic_map().copy())
+    absmax = torch.zeros((A.numel() + 63) // 64)
+    out = torch.zeros(A.numel(), dtype=torch.uint8)
+    F.lib.cquantize_blockwise_cpu_fp32(F.get_ptr(code), F.get_ptr(A), F.get_ptr(absmax), F.get_ptr(out),
+                                       ct.c_longlong(64), ct.c_longlong(A.numel()))
+    assert F.lib.cget_last_error() == 0
+    assert code[0].item() == -1.0                              # in-place side effect (cpu_ops.cpp:20)
+    assert same_bits(absmax.numpy(), golden["cpu_absmax"])
+    assert same_bits(out.numpy(), golden["cpu_q"])
+    y = torch.zeros(A.numel())
+    F.lib.cdequantize_blockwise_cpu_fp32(F.get_ptr(code), F.get_ptr(out), F.get_ptr(absmax), F.get_ptr(y),
+                                         ct.c_longlong(64), ct.c_longlong(A.numel()))
+    assert same_bits(y.numpy(), golden["cpu_deq"])
+    # the functional CPU route goes through the same entry points
+    q2, st = F.quantize_blockwise(torch.from_numpy(golden["cpu_A"].copy()), blocksize=64)
+    assert same_bits(q2.numpy(), golden["cpu_q"])
