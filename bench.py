@@ -1,0 +1,292 @@
+"""Benchmark: NF4 matmul TFLOPS (+ INT8 igemmlt TOPS) @ M=4096, N=4096, K=11008 on 1..8 MI355X.
+
+A "step" = one pass of the hot path over one batch of synthetic input:
+    nested-absmax dequant (fp32) -> fused NF4 GEMM  Y_r = X @ W_r^T  (bf16, MFMA)
+    -> RCCL all-gather of the bf16 output shards (when --gpus > 1).
+W [4096, 11008] is column-sharded by output feature across ranks (rank r owns rows
+r*N/g .. (r+1)*N/g of W, quantised NF4 bs=64 with nested statistics, the Linear4bit
+default); X [4096, 11008] bf16 is replicated.  Total work is fixed -> "scaling": "strong".
+
+Prints ONE JSON line on rank 0 (driver contract).  Extra fields: int8 igemmlt TOPS
+(metric shape and config 3 = 4096^3), the decode GEMV (config 2) GB/s, the config-1
+dequantize GB/s, the roofline of the dominant kernel and the CPU baseline.
+
+Launch:  python bench.py [--gpus 1 --steps 20 --warmup 5]
+         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as ct
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "bitsandbytes-sycl_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import python_src_quants.functional as F  # noqa: E402
+
+M, N, K = 4096, 4096, 11008
+BS = 64
+PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_INT8_TOPS = 5000.0         # dense int8 MFMA (2x bf16)
+PEAK_HBM_GBS = 8000.0           # HBM3E spec
+
+
+def _events():
+    return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+
+def _time_loop(fn, iters, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = _events()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3    # seconds per call
+
+
+def bench_int8(dev, m, n, k, iters=20):
+    """Fused igemmlt + int32->fp16 dequant (cigemmlt_row_dequant_fp16) on row-major int8 operands,
+    plus the full LLM.int8 forward (double_quant of the activations + the fused GEMM)."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    A = (torch.randn(m, k, device=dev, generator=g) * 2).half()
+    Wt = (torch.randn(n, k, device=dev, generator=g) * 0.05).half()
+    CB, _, SCB, _, _ = F.double_quant(Wt)
+    del Wt
+    CA, _, SCA, _, _ = F.double_quant(A)
+    out = torch.empty(m, n, dtype=torch.float16, device=dev)
+    t_gemm = _time_loop(lambda: F.igemmlt_dequant(CA, CB, SCA, SCB, out=out), iters)
+
+    def fwd():
+        ca, _, sca, _, _ = F.double_quant(A)
+        F.igemmlt_dequant(ca, CB, sca, SCB, out=out)
+    t_fwd = _time_loop(fwd, max(5, iters // 2))
+    ops = 2.0 * m * n * k
+    return {"shape": [m, n, k], "tops": ops / t_gemm / 1e12, "us": t_gemm * 1e6,
+            "frac_of_int8_peak": ops / t_gemm / 1e12 / PEAK_INT8_TOPS,
+            "forward_with_double_quant_us": t_fwd * 1e6}
+
+
+def bench_decode_gemv(dev, iters=60):
+    """Config 2: Linear4bit NF4 decode M=1, K=4096, N=11008, bf16, nested stats.  Rotates 14 weight copies
+    (>256 MiB) so the Infinity Cache cannot serve repeats; GB/s over the algorithmic bytes."""
+    n_out, k_in = 11008, 4096
+    copies = 14
+    g = torch.Generator(device=dev).manual_seed(2)
+    ws = []
+    for _ in range(copies):
+        W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        q, st = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=False)
+        ws.append((q, st))
+        del W
+    x = torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g)
+    out = torch.empty(1, n_out, device=dev, dtype=torch.bfloat16)
+    idx = [0]
+
+    def call():
+        q, st = ws[idx[0] % copies]
+        idx[0] += 1
+        F.gemv_4bit(x, q.t(), out=out, state=st)
+    t = _time_loop(call, iters, warmup=copies)
+    nbytes = n_out * k_in // 2 + n_out * k_in // BS * 4 + k_in * 2 + n_out * 2   # 25,392,640 B
+    return {"shape": [1, n_out, k_in], "us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS,
+            "bytes": nbytes, "note": "non-nested absmax; 14 rotating weight copies (~355 MB) defeat the 256 MB MALL"}
+
+
+def bench_dequant_config1(dev, iters=40):
+    """Config 1 on the GPU: dequantize_blockwise NF4 of a 4096x4096 weight, bs=64 -> bf16 (HBM-bound)."""
+    g = torch.Generator(device=dev).manual_seed(0)
+    copies = 8
+    qs = []
+    for _ in range(copies):
+        W = torch.randn(4096, 4096, device=dev, generator=g)
+        qs.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4"))
+    out = torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16)
+    idx = [0]
+
+    def call():
+        q, st = qs[idx[0] % copies]
+        idx[0] += 1
+        F.lib.cdequantize_blockwise_bf16_nf4(None, F.get_ptr(q), F.get_ptr(st.absmax), F.get_ptr(out), ct.c_int(BS),
+                                              ct.c_int(4096 * 4096))
+    F.pre_call(dev)
+    t = _time_loop(call, iters, warmup=copies)
+    nbytes = 42_991_616
+    return {"us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS, "bytes": nbytes}
+
+
+def cpu_baseline(rows=256):
+    """Reference CPU path as ported (oracle/cpu_ops_port.cpp, the restated cpu_ops.cpp dequantize_cpu,
+    single-threaded as written) + torch CPU F.linear (the CPU path has no GEMM), on a
+    bounded sample: the full W [4096, 11008] dequantised once, GEMM over `rows` activation rows."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from oracle.maps import nf4_padded_256
+    lib = ct.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_ops_port.so"))
+    rng = np.random.default_rng(0)
+    n_el = N * K
+    idx = rng.integers(0, 16, n_el, dtype=np.uint8)            # unpacked NF4 indices, 1 B/elem (Q17)
+    absmax = rng.uniform(0.01, 0.1, n_el // BS).astype(np.float32)
+    code = nf4_padded_256()
+    W = np.empty(n_el, np.float32)
+    t0 = time.perf_counter()
+    lib.port_dequantize_cpu(code.ctypes.data_as(ct.c_void_p), idx.ctypes.data_as(ct.c_void_p),
+                            absmax.ctypes.data_as(ct.c_void_p), W.ctypes.data_as(ct.c_void_p),
+                            ct.c_longlong(BS), ct.c_longlong(n_el))
+    t_deq = time.perf_counter() - t0
+    Wt = torch.from_numpy(W).view(N, K)
+    X = torch.randn(rows, K)
+    threads = torch.get_num_threads()
+    torch.nn.functional.linear(X[:8], Wt)
+    t0 = time.perf_counter()
+    torch.nn.functional.linear(X, Wt)
+    t_mm = time.perf_counter() - t0
+    flops = 2.0 * rows * N * K
+    # the dequant is amortised the way the GPU step amortises nothing: one dequant + one GEMM per step
+    value = flops / (t_deq + t_mm) / 1e12
+    return {"value": value, "unit": "TFLOP/s", "cores": threads, "kind": "port",
+            "sample": f"dequantize_cpu (1 thread, as ref:sycl/cpu_ops.cpp:7-14) of W[{N},{K}] NF4 bs=64 "
+                      f"({t_deq:.2f}s, {n_el * 9 / t_deq / 1e9:.2f} GB/s) + torch CPU fp32 F.linear on {rows} rows "
+                      f"({t_mm:.2f}s, {threads} threads)",
+            "dequant_cpu_gbs": n_el * 9 / t_deq / 1e9}
+
+
+def load_pmc_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        try:
+            with open(p) as f:
+                return json.load(f)
+        except Exception:  # noqa: BLE001
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-extras", action="store_true", help="skip int8/decode/config-1/cpu legs")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    assert N % world == 0
+    shard = N // world
+
+    # ---- synthetic data (same global problem for every world size)
+    gx = torch.Generator(device=dev).manual_seed(1)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=gx)
+    gw = torch.Generator(device=dev).manual_seed(1000 + rank)
+    W = (torch.randn(shard, K, device=dev, generator=gw) * 0.02).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True)
+    del W
+    Y = torch.empty(M, shard, device=dev, dtype=torch.bfloat16)
+    gathered = torch.empty(world * M, shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
+    kev = []
+
+    def step(record=False):
+        absmax = F._absmax_fp32(st)                 # nested stats -> fp32 absmax (2 small launches)
+        if record:
+            s, e = _events()
+            s.record()
+        F.gemm_4bit(X, q, st, out=Y, absmax=absmax)
+        if record:
+            e.record()
+            kev.append((s, e))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, Y)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_per_step = elapsed / args.steps * 1e3
+    total_flops = 2.0 * M * N * K
+    value = total_flops / (elapsed / args.steps) / 1e12
+    kern_s = sum(s.elapsed_time(e) for s, e in kev) / len(kev) * 1e-3
+    shard_flops = 2.0 * M * shard * K
+    achieved = shard_flops / kern_s / 1e12
+
+    extras = {}
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras["int8_igemmlt_metric_shape"] = bench_int8(dev, M, N, K)
+        extras["int8_igemmlt_config3"] = bench_int8(dev, 4096, 4096, 4096)
+        extras["decode_gemv_config2"] = bench_decode_gemv(dev)
+        extras["dequant_nf4_config1_gpu"] = bench_dequant_config1(dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and not args.no_extras:
+        try:
+            cpu = cpu_baseline()
+        except Exception as ex:  # noqa: BLE001
+            cpu = {"value": None, "unit": "TFLOP/s", "cores": None, "kind": "port", "sample": f"failed: {ex}"}
+
+    if rank == 0:
+        pmc = load_pmc_traffic()
+        traffic = None
+        if pmc and pmc.get("kernel_prefix") and pmc.get("shape") == [M, shard, K]:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        line = {
+            "metric": "NF4 matmul TFLOPS + INT8 igemmlt TOPS @ 4096x4096x11008, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "TFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (seeded randn; W ~ N(0,0.02) -> NF4 bs=64 nested stats; X ~ N(0,1) bf16)",
+            "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (fused dequant+MFMA) "
+                                   "+ bf16 all-gather of output-column shards",
+                       "M": M, "N": N, "K": K, "blocksize": BS, "quant_type": "nf4", "compress_statistics": True,
+                       "parallelism": f"column-shard x{world} + RCCL all_gather" if world > 1 else "single GPU"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                         "kernel": "k_gemm_4bit<bf16>", "kernel_us": round(kern_s * 1e6, 2),
+                         "flops_per_launch": shard_flops},
+            "cpu_baseline": cpu,
+        }
+        line.update(extras)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
