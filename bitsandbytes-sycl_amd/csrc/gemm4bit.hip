@@ -21,42 +21,13 @@
 // per workgroup through a 256-entry LDS pair table and written to LDS as T in the same
 // swizzled layout, so both MFMA operands are read with conflict-free ds_read_b128.
 // XCD-aware tile order keeps the tiles that share activation panels on one XCD's L2.
-#include "common.hpp"
+#include "gemm_common.hpp"
 
 namespace bnb {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
-typedef __attribute__((ext_vector_type(4))) float f32x4_t;
-
-template <typename T> struct Mfma;
-template <> struct Mfma<bf16_t> {
-  __device__ static __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-  }
-  __device__ static __forceinline__ uint32_t pack2(float lo, float hi) { return pack_bf16x2(lo, hi); }
-};
-template <> struct Mfma<fp16_t> {
-  __device__ static __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
-  }
-  __device__ static __forceinline__ uint32_t pack2(float lo, float hi) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, Io<fp16_t>::from_f32(lo)) |
-           ((uint32_t)__builtin_bit_cast(uint16_t, Io<fp16_t>::from_f32(hi)) << 16);
-  }
-};
-
-__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
-  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
-}
 
 constexpr int G_BM = 128, G_BN = 128, G_BK = 64, G_THREADS = 256;
 constexpr int G_TILE_BYTES = G_BM * G_BK * 2;        // 16 KiB per operand per stage
 constexpr int G_LDS_BYTES = 4 * G_TILE_BYTES + 256 * 8;
-
-// byte offset of 16-B slot s (0..7) of row r in a [rows][64] 16-bit tile, XOR swizzled
-__device__ __forceinline__ int swz(int r, int s) { return r * 128 + ((s ^ (r & 7)) << 4); }
 
 template <typename T>
 __global__ void __launch_bounds__(G_THREADS, 2)
@@ -184,6 +155,8 @@ k_gemm_4bit(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restr
   }
 }
 
+int g_tile_override = 0;
+
 template <typename T>
 void gemm_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype, T* out,
                int lda, int ldb, int ldc, int blocksize) {
@@ -193,9 +166,18 @@ void gemm_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* a
     set_error(1, "gemm_4bit: requires k % 64 == 0, lda % 8 == 0, ldb % 16 == 0, 16-B aligned A/B, blocksize >= 64");
     return;
   }
-  const int tiles = ((m + G_BN - 1) / G_BN) * ((n + G_BM - 1) / G_BM);
-  hipLaunchKernelGGL((k_gemm_4bit<T>), dim3(tiles), dim3(G_THREADS), 0, current_stream(), m, n, k, A, B, absmax,
-                     datatype, out, lda, ldb, ldc, blocksize);
+  // m = out features (weight rows), n = tokens.  Large problems: 256x256 tiles; small: 128x128.
+  const long long tiles256 = (long long)((m + 255) / 256) * ((n + 255) / 256);
+  const bool pow2_bs = (blocksize & (blocksize - 1)) == 0;
+  const bool use256 = pow2_bs && (g_tile_override == 256 ||
+                                  (g_tile_override != 128 && m >= 256 && n >= 256 && tiles256 >= 128));
+  if (use256) {
+    launch_gemm_4bit_256<T>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
+  } else {
+    const int tiles = ((m + G_BN - 1) / G_BN) * ((n + G_BM - 1) / G_BM);
+    hipLaunchKernelGGL((k_gemm_4bit<T>), dim3(tiles), dim3(G_THREADS), 0, current_stream(), m, n, k, A, B, absmax,
+                       datatype, out, lda, ldb, ldc, blocksize);
+  }
   BNB_LAUNCH_CHECK("gemm_4bit");
 }
 
@@ -237,3 +219,8 @@ void cgemm_4bit_inference_code_bf16(int m, int n, int k, bf16_t* A, unsigned cha
 }
 
 }  // extern "C"
+
+extern "C" {
+// [additive, testing] force the tile kernel used by the 4-bit GEMM (0 = auto, 128 = 128x128 kernel)
+void cgemm_4bit_set_tile(int tile) { bnb::g_tile_override = tile; }
+}

@@ -1,0 +1,190 @@
+// 256 x 256-tile fused 4-bit weight GEMM (the large-problem kernel behind cgemm_4bit_inference*,
+// see gemm4bit.hip for the ABI / semantics; ref:sycl/pythonInterface.cpp:377-378, kernel_gemm.cpp:1015).
+//
+// Geometry: 512 threads = 8 waves (2 along tokens x 4 along out-features), 128 x 64 outputs per wave
+// (8 x 4 tiles of v_mfma_f32_16x16x32), BK = 64, one workgroup per CU (148 KiB LDS).
+//
+// Every operand arrives by LDS-DMA (global_load_lds), so no VGPR-destination load is ever in flight
+// in the k-loop (hipcc otherwise drains the prefetch early, cdna_hip_programming.md §5):
+//   Xs[2]  activations   2 x 32 KiB  [256][64] T, XOR-swizzled through the source address
+//   Ws[2]  weights (T)   2 x 32 KiB  same layout, written by the in-kernel dequantisation
+//   Wp[2]  packed 4-bit  2 x  8 KiB  [256 rows][2 halves][16 B], lane-linear
+//   Am[2]  absmax        2 x  1 KiB  one fp32 per weight row and k-step (bs >= 64)
+//   LUT                      2 KiB   byte -> {code[hi], code[lo]}
+// k-step t (one barrier): DMA X(t+1), W(t+2) packed, absmax(t+2); 64 MFMAs per wave on stage t,
+// interleaved with the dequantisation of W(t+1) (Wp -> LUT -> *absmax -> one RNE cast -> Ws);
+// vmcnt(0) + barrier.  The body is branch-free (prefetch indices are clamped) so the scheduler can
+// interleave the dequant VALU/LDS work between the MFMAs.
+#include "gemm_common.hpp"
+
+namespace bnb {
+
+constexpr int Q_BM = 256, Q_BN = 256, Q_BK = 64, Q_THREADS = 512;
+constexpr int Q_XT = Q_BM * Q_BK * 2;          // 32 KiB
+constexpr int Q_WT = Q_BN * Q_BK * 2;          // 32 KiB
+constexpr int Q_PT = Q_BN * Q_BK / 2;          // 8 KiB
+constexpr int Q_AT = 2 * Q_BN * 4;             // 2 KiB (absmax + spare copy)
+constexpr int Q_OFF_X = 0;
+constexpr int Q_OFF_W = 2 * Q_XT;
+constexpr int Q_OFF_P = Q_OFF_W + 2 * Q_WT;
+constexpr int Q_OFF_A = Q_OFF_P + 2 * Q_PT;
+constexpr int Q_OFF_L = Q_OFF_A + 2 * Q_AT;
+constexpr int Q_LDS = Q_OFF_L + 256 * 8;       // 151,552 B
+constexpr int Q_EPI_STRIDE = 136;              // staged output row: 128 B + 8 B pad
+static_assert(8 * 128 * Q_EPI_STRIDE <= Q_OFF_L, "epilogue staging must not overlap the LUT");
+
+template <typename T>
+__device__ __forceinline__ void dequant_slot_pair(uint8_t* ws, const float2* lut, uint32_t w0, uint32_t w1, float am,
+                                                  int row, int slot0) {
+  const uint32_t w[2] = {w0, w1};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    uint32_t pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float2 c = lut[(w[s] >> (8 * j)) & 0xFF];
+      pk[j] = Mfma<T>::pack2(__fmul_rn(c.x, am), __fmul_rn(c.y, am));
+    }
+    *reinterpret_cast<uint4*>(ws + swz(row, slot0 + s)) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(Q_THREADS, 1)
+k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B,
+                const float* __restrict__ absmax, const float* __restrict__ datatype, T* __restrict__ out,
+                int lda, int ldb, int ldc, int blocksize) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[Q_LDS];
+  float2* lut = reinterpret_cast<float2*>(smem + Q_OFF_L);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 256) lut[tid] = make_float2(datatype[tid >> 4], datatype[tid & 15]);
+
+  // ---- tile order: XCD-contiguous ids, grouped 4 token-tiles x all feature-tiles
+  const int tilesN = (N + Q_BN - 1) / Q_BN, tilesM = (M + Q_BM - 1) / Q_BM;
+  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  constexpr int GROUP = 4;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * Q_BM, n0 = tn * Q_BN;
+
+  // ---- DMA source addresses (k = 0); per k-step they advance by 64 elements / 32 bytes
+  const T* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wave + i) + (lane >> 3);
+    xsrc[i] = A + (long long)min(m0 + row, M - 1) * lda + 8 * ((lane & 7) ^ (row & 7));
+  }
+  const int prow = tid >> 1, phalf = tid & 1;                       // this lane's packed 16 B
+  const uint8_t* psrc = B + (long long)min(n0 + prow, N - 1) * ldb + 16 * phalf;
+  // absmax DMA: one row per lane; waves 4-7 repeat waves 0-3 into the stage's spare copy (branch-free)
+  const int arow = 64 * (wave & 3) + lane;
+  const int bs_shift = __builtin_ctz(blocksize);                    // blocksize: power of two >= 64
+  const long long abase = 2LL * ldb * min(n0 + arow, N - 1);        // element index of (row, k = 0)
+
+  const int nk = K / Q_BK;
+  auto dma_w = [&](int kt, int buf) {                               // packed weights + absmax of k-tile kt
+    glds16(psrc + (long long)kt * (Q_BK / 2), smem + Q_OFF_P + buf * Q_PT + wave * 1024);
+    glds4(absmax + ((abase + (long long)kt * Q_BK) >> bs_shift), smem + Q_OFF_A + buf * Q_AT + wave * 256);
+  };
+  auto dma_x = [&](int kt, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16(xsrc[i] + (long long)kt * Q_BK, smem + Q_OFF_X + buf * Q_XT + (4 * wave + i) * 1024);
+  };
+  auto dequant_half = [&](int buf_src, int buf_dst, int h) {       // h = 0/1: first/second 8 packed bytes
+    const uint8_t* p = smem + Q_OFF_P + buf_src * Q_PT + 16 * tid;
+    const uint2 w = *reinterpret_cast<const uint2*>(p + 8 * h);
+    const float am = *reinterpret_cast<const float*>(smem + Q_OFF_A + buf_src * Q_AT + 4 * prow);
+    dequant_slot_pair<T>(smem + Q_OFF_W + buf_dst * Q_WT, lut, w.x, w.y, am, prow, 4 * phalf + 2 * h);
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: X(0), W(0), W(1) in flight; dequantise W(0) into Ws[0]
+  dma_x(0, 0);
+  dma_w(0, 0);
+  dma_w(min(1, nk - 1), 1);
+  wait_vmcnt0();
+  __syncthreads();
+  dequant_half(0, 0, 0);
+  dequant_half(0, 0, 1);
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    dma_x(min(t + 1, nk - 1), s ^ 1);
+    dma_w(min(t + 2, nk - 1), s);
+    const uint8_t* xs = smem + Q_OFF_X + s * Q_XT;
+    const uint8_t* ws = smem + Q_OFF_W + s * Q_WT;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int slot = 4 * ks + (lane >> 4);
+      uint4 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(ws + swz(64 * wn + 16 * j + (lane & 15), slot));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint4 a = *reinterpret_cast<const uint4*>(xs + swz(128 * wm + 16 * i + (lane & 15), slot));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = Mfma<T>::mma(a, b[j], acc[i][j]);
+      }
+      dequant_half(s ^ 1, s ^ 1, ks);   // W(t+1): Wp[(t+1)&1] -> Ws[(t+1)&1]
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  // ---- epilogue: acc -> LDS (per-wave [128][64] T, 136-B rows) -> 16-B coalesced stores
+  uint8_t* ep = smem + wave * (128 * Q_EPI_STRIDE);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * (lane >> 4) + r, col = 16 * j + (lane & 15);
+        *reinterpret_cast<T*>(ep + row * Q_EPI_STRIDE + 2 * col) = Io<T>::from_f32(acc[i][j][r]);
+      }
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the wave reads back only its own region
+  const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;
+  const bool vec_ok = ((ldc & 7) == 0) && (((uintptr_t)out & 15) == 0);
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = lane + 64 * it;
+    const int row = id >> 3, c8 = id & 7;
+    const int grow = grow0 + row, gcol = gcol0 + 8 * c8;
+    if (grow >= M) continue;
+    const uint2 lo = *reinterpret_cast<const uint2*>(ep + row * Q_EPI_STRIDE + 16 * c8);
+    const uint2 hi = *reinterpret_cast<const uint2*>(ep + row * Q_EPI_STRIDE + 16 * c8 + 8);
+    T* dst = out + (long long)grow * ldc + gcol;
+    if (vec_ok && gcol + 8 <= N) {
+      *reinterpret_cast<uint4*>(dst) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    } else {
+      const uint32_t w4[4] = {lo.x, lo.y, hi.x, hi.y};
+      for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = __builtin_bit_cast(T, (uint16_t)(w4[e >> 1] >> (16 * (e & 1))));
+    }
+  }
+}
+
+template <typename T>
+void launch_gemm_4bit_256(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype,
+                          T* out, int lda, int ldb, int ldc, int blocksize) {
+  const long long tiles = (long long)((m + Q_BN - 1) / Q_BN) * ((n + Q_BM - 1) / Q_BM);
+  hipLaunchKernelGGL((k_gemm_4bit_256<T>), dim3((unsigned)tiles), dim3(Q_THREADS), 0, current_stream(), m, n, k, A, B,
+                     absmax, datatype, out, lda, ldb, ldc, blocksize);
+}
+
+template void launch_gemm_4bit_256<bf16_t>(int, int, int, const bf16_t*, const uint8_t*, const float*, const float*,
+                                           bf16_t*, int, int, int, int);
+template void launch_gemm_4bit_256<fp16_t>(int, int, int, const fp16_t*, const uint8_t*, const float*, const float*,
+                                           fp16_t*, int, int, int, int);
+
+}  // namespace bnb

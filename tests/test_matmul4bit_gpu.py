@@ -110,6 +110,48 @@ def test_gemm_4bit_vs_oracle(dev, dtype, qt, mnk):
     assert (Y.float() - Yref).abs().mean().item() < 0.115
 
 
+@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("mnk", [(256, 256, 128), (300, 520, 640), (1000, 384, 256)])
+def test_gemm_4bit_each_tile_kernel(dev, tile, mnk):
+    """Force each tile kernel (128x128 / 256x256) on shapes with ragged M/N tails."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M + N + K)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
+    F.lib.cgemm_4bit_set_tile(tile)
+    try:
+        Y = F.gemm_4bit(X, q, st)
+    finally:
+        F.lib.cgemm_4bit_set_tile(0)
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), st.absmax.cpu().numpy(), N, K, 64,
+                                    st.code.cpu().numpy(), "bf16")
+    frac, err = _close(Y.float().cpu().numpy(), exp, 2e-2, 2e-2)
+    assert frac == 0.0, err
+
+
+def test_gemm_4bit_tile_kernels_agree_large(dev):
+    """Metric shape class: the 256x256 kernel (auto) equals the 128x128 kernel up to fp32 summation order."""
+    F = _F()
+    M, N, K = 2048, 2048, 11008
+    torch.manual_seed(11)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    Y = F.gemm_4bit(X, q, st)
+    F.lib.cgemm_4bit_set_tile(128)
+    try:
+        Y1 = F.gemm_4bit(X, q, st)
+    finally:
+        F.lib.cgemm_4bit_set_tile(0)
+    Wd = F.dequantize_4bit(q, st)
+    Yref = X.float() @ Wd.float().t()
+    rms = Yref.pow(2).mean().sqrt().item()
+    assert (Y.float() - Yref).abs().max().item() < 2e-2 * rms + 2e-2 * Yref.abs().max().item()
+    assert (Y.float() - Y1.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Yref.abs().max().item()
+
+
 def test_gemm_4bit_legacy_abi_nf4_fp16(dev):
     """cgemm_4bit_inference (ref ABI slot, fp16, NF4 hard-coded)."""
     F = _F()

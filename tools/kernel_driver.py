@@ -1,0 +1,52 @@
+"""Run one hot-path kernel repeatedly (for rocprofv3 counter passes / A-B timing on the GPU box).
+Usage: python tools/kernel_driver.py {nf4gemm,int8gemm,gemv,dequant} [iters]"""
+import ctypes as ct
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "bitsandbytes-sycl_amd")]
+import torch  # noqa: E402
+import python_src_quants.functional as F  # noqa: E402
+
+
+def main():
+    what = sys.argv[1]
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    if what == "nf4gemm":
+        M, N, K = 4096, 4096, 11008
+        X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
+        Y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        fn = lambda: F.gemm_4bit(X, q, st, out=Y, absmax=st.absmax)  # noqa: E731
+        flops = 2.0 * M * N * K
+    elif what == "int8gemm":
+        M, N, K = 4096, 4096, 11008
+        A = torch.randint(-127, 128, (M, K), device=dev, dtype=torch.int8)
+        B = torch.randint(-127, 128, (N, K), device=dev, dtype=torch.int8)
+        rs = torch.rand(M, device=dev) + 0.5
+        cs = torch.rand(N, device=dev) + 0.5
+        out = torch.empty(M, N, device=dev, dtype=torch.float16)
+        fn = lambda: F.igemmlt_dequant(A, B, rs, cs, out=out)  # noqa: E731
+        flops = 2.0 * M * N * K
+    else:
+        raise SystemExit(f"unknown {what}")
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / iters * 1e-3
+    print(f"{what}: {t*1e6:.1f} us/call, {flops / t / 1e12:.1f} T(FL)OP/s")
+
+
+if __name__ == "__main__":
+    main()
