@@ -33,18 +33,32 @@ constexpr int Q_LDS = Q_OFF_L + 256 * 8;       // 151,552 B
 constexpr int Q_EPI_STRIDE = 136;              // staged output row: 128 B + 8 B pad
 static_assert(8 * 128 * Q_EPI_STRIDE <= Q_OFF_L, "epilogue staging must not overlap the LUT");
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// one packed byte -> {T(code[hi]*am), T(code[lo]*am)} as a dword: ds_read_b64 of the pair table,
+// v_pk_mul_f32 by the broadcast absmax, one v_cvt_pk (RNE) -- the reference's dequantised values.
+template <typename T> __device__ __forceinline__ uint32_t deq_byte(const f32x2_t* lut, uint32_t byte, f32x2_t am2);
+template <> __device__ __forceinline__ uint32_t deq_byte<bf16_t>(const f32x2_t* lut, uint32_t byte, f32x2_t am2) {
+  const f32x2_t p = lut[byte] * am2;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2_t));
+}
+template <> __device__ __forceinline__ uint32_t deq_byte<fp16_t>(const f32x2_t* lut, uint32_t byte, f32x2_t am2) {
+  const f32x2_t p = lut[byte] * am2;
+  return Mfma<fp16_t>::pack2(p.x, p.y);
+}
+
 template <typename T>
 __device__ __forceinline__ void dequant_slot_pair(uint8_t* ws, const float2* lut, uint32_t w0, uint32_t w1, float am,
                                                   int row, int slot0) {
   const uint32_t w[2] = {w0, w1};
+  const f32x2_t am2 = {am, am};
+  const f32x2_t* lut2 = reinterpret_cast<const f32x2_t*>(lut);
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     uint32_t pk[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float2 c = lut[(w[s] >> (8 * j)) & 0xFF];
-      pk[j] = Mfma<T>::pack2(__fmul_rn(c.x, am), __fmul_rn(c.y, am));
-    }
+    for (int j = 0; j < 4; ++j) pk[j] = deq_byte<T>(lut2, (w[s] >> (8 * j)) & 0xFF, am2);
     *reinterpret_cast<uint4*>(ws + swz(row, slot0 + s)) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
   }
 }
@@ -56,7 +70,8 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
                 int lda, int ldb, int ldc, int blocksize) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[Q_LDS];
   float2* lut = reinterpret_cast<float2*>(smem + Q_OFF_L);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);        // provably wave-uniform (SGPR math)
   if (tid < 256) lut[tid] = make_float2(datatype[tid >> 4], datatype[tid & 15]);
 
   // ---- tile order: XCD-contiguous ids, grouped 4 token-tiles x all feature-tiles
