@@ -83,6 +83,8 @@ void cgemm_4bit_inference_code_fp16(int m, int n, int k, bnb_fp16* A, unsigned c
                                     bnb_fp16* out, int lda, int ldb, int ldc, int blocksize);
 void cgemm_4bit_inference_code_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, float* absmax, float* datatype,
                                     bnb_bf16* out, int lda, int ldb, int ldc, int blocksize);
+/* [additive, testing] force the GEMM tile kernel: 0 = auto, 128 = 128x128, 256 = 256x256 */
+void cgemm_4bit_set_tile(int tile);
 
 /* ---- LLM.int8 statistics and quantisation: ref:sycl/pythonInterface.cpp:333-339 ---- */
 void cget_col_row_stats(bnb_fp16* A, float* rowStats, float* colStats, int* nnz_count_row, float nnz_threshold, int rows,

@@ -1,0 +1,71 @@
+"""World-size-2 gloo test of the column-shard + all-gather logic (CPU, no GPU compute).
+
+Each rank slices its rows out of a full 4-bit quantised weight with the product's
+`shard_packed_rows`, computes its [M, N/2] output slice with the oracle (test-side compute),
+and the product's `gather_columns` / `gathered_to_rows` assemble [M, N]; the result must equal
+the unsharded oracle output bit-for-bit, and each slice must equal quantising the shard alone.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, ret):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "bitsandbytes-sycl_amd")]
+    from oracle import ref
+    from python_src_quants.parallel import gather_columns, gathered_to_rows, shard_packed_rows, shard_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, K, M, bs = 96, 256, 5, 64
+        rng = np.random.default_rng(0)
+        W = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+        X = rng.standard_normal((M, K)).astype(np.float32)
+        absmax, q = ref.quantize_blockwise(W.reshape(-1), bs, "nf4")
+        start, end = shard_range(N, world, rank)
+        p, a = shard_packed_rows(torch.from_numpy(q).reshape(-1, 1), torch.from_numpy(absmax), (N, K), bs, start, end)
+        a_s, q_s = ref.quantize_blockwise(W[start:end].reshape(-1), bs, "nf4")
+        assert np.array_equal(p.numpy().reshape(-1), q_s) and np.array_equal(a.numpy(), a_s)
+        y_local = ref.gemm_4bit_dequant_ref(X, p.numpy(), a.numpy(), end - start, K, bs, ref.nf4_table(), "fp32")
+        g = gather_columns(torch.from_numpy(y_local.astype(np.float32)), world)
+        full = gathered_to_rows(g).numpy()
+        exp = ref.gemm_4bit_dequant_ref(X, q, absmax, N, K, bs, ref.nf4_table(), "fp32").astype(np.float32)
+        ret[rank] = bool(np.array_equal(full, exp))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_column_shard_allgather_gloo(world):
+    port = _free_port()
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(world, port, ret), nprocs=world, join=True)
+    assert dict(ret) == {r: True for r in range(world)}
+
+
+def test_shard_range_errors():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "bitsandbytes-sycl_amd")]
+    from python_src_quants.parallel import shard_range
+    assert shard_range(4096, 8, 7) == (3584, 4096)
+    with pytest.raises(ValueError):
+        shard_range(100, 8, 0)
