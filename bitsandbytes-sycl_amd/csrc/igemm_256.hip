@@ -1,0 +1,198 @@
+// 256 x 256-tile int8 GEMM on v_mfma_i32_16x16x64_i8 (gfx950): the large-problem kernel behind
+// igemmlt (ref:sycl/sycl_code/op_gemm.cpp:541-655, C = A @ B^T exact int32) and the fused
+// igemmlt + dequant_mm_int32_fp16 path (ref:sycl/sycl_code/kernel_quant.cpp:3846-3987).
+//
+// Geometry: 512 threads = 8 waves (2 along M x 4 along N), 128 x 64 outputs per wave (8 x 4 tiles of
+// 16x16), BK = 128 bytes, two LDS stages (2 x (32 + 32) KiB), one barrier per k-step.  Both operands
+// arrive by LDS-DMA (16 B per lane, XOR-swizzled through the source address) from any layout whose
+// 16-k runs are contiguous: row-major, col32 (A) and col_ampere (B).  Fragment convention: lane l
+// holds 16 consecutive k of row l&15, k-chunk l>>4 -- identical for A and B, so the int32 result is
+// exact whatever order the instruction sums k in.  Epilogues: int32 row-major / col32, int8 col32
+// (alpha = 1 or per-row scale) and the fused mm_dequant to fp16, staged through LDS for 16-B stores.
+#include "gemm_common.hpp"
+#include "int8_common.hpp"
+
+namespace bnb {
+
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+
+constexpr int J_BM = 256, J_BN = 256, J_BK = 128, J_THREADS = 512;
+constexpr int J_TILE = J_BM * J_BK;                     // 32 KiB
+constexpr int J_EPI_STRIDE = 136;                       // fp16 staging row: 128 B + 8 B pad
+constexpr int J_LDS_MAIN = 4 * J_TILE;                  // 128 KiB
+constexpr int J_LDS_EPI = 8 * 128 * J_EPI_STRIDE;       // 136 KiB
+constexpr int J_LDS = J_LDS_MAIN > J_LDS_EPI ? J_LDS_MAIN : J_LDS_EPI;
+
+template <int F>
+__device__ __forceinline__ const int8_t* chunk_ptr(const int8_t* P, long long ld, long long r, long long k) {
+  return P + fmt_offset<F>(r, k, ld);    // 16 contiguous bytes for ROW / COL32 / AMPERE when k % 16 == 0
+}
+
+template <int AF, int BF, int EPI>
+__global__ void __launch_bounds__(J_THREADS, 1)
+k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restrict__ B, void* __restrict__ Cout,
+            const float* __restrict__ row_scale, long long lda, long long ldb, long long ldc,
+            const float* __restrict__ rowStats, const float* __restrict__ colStats, const fp16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[J_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int tilesN = (N + J_BN - 1) / J_BN, tilesM = (M + J_BM - 1) / J_BM;
+  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  constexpr int GROUP = 4;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * J_BM, n0 = tn * J_BN;
+
+  // DMA roles: wave-instruction i covers tile rows 8*(4*wave+i) .. +7, lane -> (row, 16-B slot)
+  long long arow[4], brow[4];
+  int kslot[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wave + i) + (lane >> 3);
+    arow[i] = min(m0 + row, M - 1);
+    brow[i] = min(n0 + row, N - 1);
+    kslot[i] = 16 * ((lane & 7) ^ (row & 7));
+  }
+  auto dma = [&](int kt, int buf) {
+    const long long k0 = (long long)kt * J_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(chunk_ptr<AF>(A, lda, arow[i], k0 + kslot[i]), smem + buf * J_TILE + (4 * wave + i) * 1024);
+      glds16(chunk_ptr<BF>(B, ldb, brow[i], k0 + kslot[i]), smem + 2 * J_TILE + buf * J_TILE + (4 * wave + i) * 1024);
+    }
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  i32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = i32x4_t{0, 0, 0, 0};
+
+  const int nk = K / J_BK;
+  dma(0, 0);
+  wait_vmcnt0();
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    dma(min(t + 1, nk - 1), s ^ 1);
+    const uint8_t* as = smem + s * J_TILE;
+    const uint8_t* bs = smem + 2 * J_TILE + s * J_TILE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int slot = 4 * ks + (lane >> 4);
+      uint4 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz(64 * wn + 16 * j + (lane & 15), slot));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint4 a = *reinterpret_cast<const uint4*>(as + swz(128 * wm + 16 * i + (lane & 15), slot));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a), __builtin_bit_cast(i32x4_t, b[j]),
+                                                            acc[i][j], 0, 0, 0);
+      }
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  // ---- epilogues (C/D: col = lane&15, row = 4*(lane>>4) + r)
+  const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;
+  if constexpr (EPI == EPI_F16_ROW_DEQUANT) {
+    uint8_t* ep = smem + wave * (128 * J_EPI_STRIDE);
+    float cs[4], bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = min(gcol0 + 16 * j + (lane & 15), N - 1);
+      cs[j] = colStats[col];
+      bv[j] = bias ? (float)bias[col] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * (lane >> 4) + r;
+        const float rs = rowStats[min(grow0 + row, M - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<fp16_t*>(ep + row * J_EPI_STRIDE + 2 * (16 * j + (lane & 15))) =
+              mm_dequant_value(acc[i][j][r], rs, cs[j], bv[j]);
+      }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    fp16_t* out = reinterpret_cast<fp16_t*>(Cout);
+    const bool vec_ok = ((ldc & 7) == 0) && (((uintptr_t)out & 15) == 0);
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int id = lane + 64 * it;
+      const int row = id >> 3, c8 = id & 7;
+      const int grow = grow0 + row, gcol = gcol0 + 8 * c8;
+      if (grow >= M) continue;
+      const uint2 lo = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8 + 8);
+      fp16_t* dst = out + (long long)grow * ldc + gcol;
+      if (vec_ok && gcol + 8 <= N) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      } else {
+        const uint32_t w4[4] = {lo.x, lo.y, hi.x, hi.y};
+        for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = __builtin_bit_cast(fp16_t, (uint16_t)(w4[e >> 1] >> (16 * (e & 1))));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = grow0 + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= M) continue;
+        float rsc = 1.0f;
+        if constexpr (EPI == EPI_I8_COL32_ROWSCALE) rsc = row_scale[row];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = gcol0 + 16 * j + (lane & 15);
+          if (col >= N) continue;
+          const int32_t v = acc[i][j][r];
+          if constexpr (EPI == EPI_I32_ROW) reinterpret_cast<int32_t*>(Cout)[(long long)row * ldc + col] = v;
+          else if constexpr (EPI == EPI_I32_COL32) reinterpret_cast<int32_t*>(Cout)[fmt_offset<COL32>(row, col, ldc)] = v;
+          else if constexpr (EPI == EPI_I8_COL32) reinterpret_cast<int8_t*>(Cout)[fmt_offset<COL32>(row, col, ldc)] = rint_i8((float)v);
+          else reinterpret_cast<int8_t*>(Cout)[fmt_offset<COL32>(row, col, ldc)] = rint_i8(__fmul_rn((float)v, rsc));
+        }
+      }
+  }
+}
+
+template <int AF, int BF, int EPI>
+bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale,
+                      long long lda, long long ldb, long long ldc, const float* rowStats, const float* colStats,
+                      const fp16_t* bias) {
+  if constexpr (AF == TURING || BF == TURING) {
+    return false;                                                  // 4-byte runs: register-staged kernel
+  } else {
+    if (k % J_BK != 0 || m < 256 || n < 256) return false;
+    if ((AF == ROW && lda % 16) || (BF == ROW && ldb % 16) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return false;
+    const long long tiles = (long long)((m + J_BM - 1) / J_BM) * ((n + J_BN - 1) / J_BN);
+    hipLaunchKernelGGL((k_igemm_256<AF, BF, EPI>), dim3((unsigned)tiles), dim3(J_THREADS), 0, current_stream(), m, n,
+                       k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias);
+    return true;
+  }
+}
+
+#define BNB_INST(AF, BF, EPI)                                                                                      \
+  template bool launch_igemm_256<AF, BF, EPI>(int, int, int, const int8_t*, const int8_t*, void*, const float*,    \
+                                              long long, long long, long long, const float*, const float*,         \
+                                              const fp16_t*);
+BNB_INST(ROW, ROW, EPI_F16_ROW_DEQUANT)
+BNB_INST(ROW, ROW, EPI_I32_ROW)
+BNB_INST(COL32, AMPERE, EPI_I32_COL32)
+BNB_INST(COL32, AMPERE, EPI_I8_COL32)
+BNB_INST(COL32, AMPERE, EPI_I8_COL32_ROWSCALE)
+BNB_INST(COL32, TURING, EPI_I32_COL32)
+BNB_INST(COL32, TURING, EPI_I8_COL32)
+BNB_INST(COL32, TURING, EPI_I8_COL32_ROWSCALE)
+#undef BNB_INST
+
+}  // namespace bnb

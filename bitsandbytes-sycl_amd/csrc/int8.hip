@@ -16,25 +16,9 @@
 //   col32      (c/32)*ld + 32 r + c%32                                  ld = 32*rows
 //   col_turing (c/32)*ld + (r/8)*256 + 128(r%2) + 16((c%32)/4) + 4((r%8)/2) + c%4     ld = 32*pad8(rows)
 //   col_ampere (c/32)*ld + (r/32)*1024 + 32*arow(r%32) + c%32, arow(x) = 8((x%8)/2) + 2(x/8) + x%2   ld = 32*pad32(rows)
-#include "common.hpp"
+#include "int8_common.hpp"
 
 namespace bnb {
-
-enum Fmt { ROW = 0, COL32 = 2, TURING = 3, AMPERE = 4 };
-
-__host__ __device__ __forceinline__ long long pad_to(long long v, long long m) { return (v + m - 1) / m * m; }
-
-__device__ __forceinline__ int ampere_row(int x) { return 8 * ((x & 7) >> 1) + 2 * (x >> 3) + (x & 1); }
-
-// offset of element (r, c) in format F, `ld` = the format's leading dimension (see header)
-template <int F>
-__device__ __forceinline__ long long fmt_offset(long long r, long long c, long long ld) {
-  if constexpr (F == ROW) return r * ld + c;
-  else if constexpr (F == COL32) return (c >> 5) * ld + 32 * r + (c & 31);
-  else if constexpr (F == TURING)
-    return (c >> 5) * ld + (r >> 3) * 256 + 128 * (r & 1) + 16 * ((c & 31) >> 2) + 4 * ((r & 7) >> 1) + (c & 3);
-  else return (c >> 5) * ld + (r >> 5) * 1024 + 32 * ampere_row((int)(r & 31)) + (c & 31);
-}
 
 // ============================================================================ row/col statistics
 // Tile: 16 rows x 256 cols per 256-thread workgroup (the reference's TILE_ROWS/TILE_COLS, which also
@@ -123,14 +107,6 @@ k_colrow_stats(const fp16_t* __restrict__ A, float* __restrict__ rowStats, float
 }
 
 // ============================================================================ double row/col quant
-
-__device__ __forceinline__ int8_t rint_i8(float v) {
-  // (char)rint(v): half-to-even; NaN -> 0; saturating (|v| <= 127 for in-range data)
-  float r = rintf(v);
-  if (r != r) r = 0.0f;
-  r = fminf(fmaxf(r, -128.0f), 127.0f);
-  return (int8_t)(int)r;
-}
 
 template <bool SPARSE>
 __global__ void __launch_bounds__(256)
@@ -221,16 +197,6 @@ static void launch_transform(const int8_t* A, int8_t* out, int rows, int cols) {
 
 // ============================================================================ dequant_mm_int32_fp16
 
-// out[r, c] = half( ((float(C[r,c]) * 6.200012e-05f) * rowStats[r]) * colStats[c] + bias[c] )
-// (kernel_quant.cpp:3969 operation order; explicit _rn ops forbid FMA contraction)
-__device__ __forceinline__ fp16_t mm_dequant_value(int32_t acc, float rs, float cs, float bias) {
-  float v = __fmul_rn((float)acc, 6.200012e-05f);
-  v = __fmul_rn(v, rs);
-  v = opaque(__fmul_rn(v, cs));   // keep mul and add separately rounded (no v_fma_mix fold)
-  v = __fadd_rn(v, bias);
-  return Io<fp16_t>::from_f32(v);
-}
-
 // C in col32 layout (the reference's igemmlt output, ldc = 32*numRows); 4 consecutive columns per thread
 __global__ void __launch_bounds__(256)
 k_dequant_mm_col32(const int32_t* __restrict__ C, const float* __restrict__ rowStats, const float* __restrict__ colStats,
@@ -260,7 +226,6 @@ k_dequant_mm_col32(const int32_t* __restrict__ C, const float* __restrict__ rowS
 
 typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 
-enum Epi { EPI_I32_COL32 = 0, EPI_I8_COL32 = 1, EPI_I8_COL32_ROWSCALE = 2, EPI_F16_ROW_DEQUANT = 3, EPI_I32_ROW = 4 };
 
 constexpr int Q_BM = 128, Q_BN = 128, Q_BK = 128, Q_THREADS = 256;
 constexpr int Q_TILE = Q_BM * Q_BK;   // 16 KiB
@@ -395,11 +360,20 @@ k_igemm(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restr
   }
 }
 
+static int g_igemm_tile = 0;   // 0 = auto, 128 = force the 128x128 register-staged kernel (tests / A-B)
+
 template <int AF, int BF, int EPI>
 static int launch_igemm(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale, long long lda,
                         long long ldb, long long ldc, const float* rowStats = nullptr, const float* colStats = nullptr,
                         const fp16_t* bias = nullptr) {
   if (m <= 0 || n <= 0 || k <= 0) return 0;
+  // large problems: 256x256 LDS-DMA kernel (igemm_256.hip); small / col_turing / ragged-k: 128x128 here
+  if (g_igemm_tile != 128 &&
+      launch_igemm_256<AF, BF, EPI>(m, n, k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias)) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_error((int)e, "igemmlt launch"); return 1; }
+    return 0;
+  }
   const int tiles = ((m + Q_BM - 1) / Q_BM) * ((n + Q_BN - 1) / Q_BN);
   hipLaunchKernelGGL((k_igemm<AF, BF, EPI>), dim3(tiles), dim3(Q_THREADS), 0, current_stream(), m, n, k, A, B, C,
                      row_scale, lda, ldb, ldc, rowStats, colStats, bias);
@@ -522,5 +496,8 @@ void cextractOutliers_ampere(char* A, int* idx, char* out, int idx_size, int row
                      (int8_t*)out, idx_size, rows, cols);
   BNB_LAUNCH_CHECK("extract_outliers");
 }
+
+// [additive, testing] 0 = auto, 128 = force the 128x128 int8 GEMM kernel
+void cigemm_set_tile(int tile) { g_igemm_tile = tile; }
 
 }  // extern "C"

@@ -117,6 +117,8 @@ int cigemmlt_ampere_8(int m, int n, int k, const int8_t* A, const int8_t* B, voi
 int cigemmlt_row_dequant_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, bnb_fp16* out, const float* rowStats,
                               const float* colStats, const bnb_fp16* bias, int lda, int ldb, int ldc);
 int cigemm_row_i32(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc);
+/* [additive, testing] force the int8 GEMM tile kernel: 0 = auto (256x256 when it applies), 128 = 128x128 */
+void cigemm_set_tile(int tile);
 
 /* ---- int32 -> fp16 dequant: ref:sycl/pythonInterface.cpp:333 ----
  * out[r, c] = half(((float(C[r,c]) * 6.200012e-05f) * rowStats[r]) * colStats[c] + bias[c]), C in col32 */

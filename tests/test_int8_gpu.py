@@ -85,7 +85,8 @@ def test_transforms_golden(golden, dev):
 
 
 @pytest.mark.parametrize("formatB", ["col_turing", "col_ampere"])
-@pytest.mark.parametrize("mnk", [(64, 40, 96), (4096, 4096, 4096), (1, 1, 1), (77, 300, 1000), (256, 129, 128)])
+@pytest.mark.parametrize("mnk", [(64, 40, 96), (4096, 4096, 4096), (1, 1, 1), (77, 300, 1000), (256, 129, 128),
+                                 (300, 520, 256)])
 def test_igemmlt_exact(dev, formatB, mnk):
     F = _F()
     m, n, k = mnk
@@ -144,7 +145,8 @@ def test_igemmlt_int8_out(dev):
     assert np.array_equal(got, ref.igemmlt_int8_out(A, B, scale.cpu().numpy()))
 
 
-@pytest.mark.parametrize("mnk", [(4096, 4096, 4096), (300, 200, 448), (1, 64, 128), (129, 257, 1000)])
+@pytest.mark.parametrize("mnk", [(4096, 4096, 4096), (300, 200, 448), (1, 64, 128), (129, 257, 1000),
+                                 (520, 300, 384), (4096, 4096, 11008)])
 def test_igemmlt_row_dequant_fused(dev, mnk):
     F = _F()
     m, n, k = mnk
