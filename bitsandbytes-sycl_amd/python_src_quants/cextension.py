@@ -37,7 +37,8 @@ class BNBNativeLibrary:
         lib.cget_last_error_message.restype = ct.c_char_p
         for name in ("cigemmlt_turing_32", "cigemmlt_turing_8", "cigemmlt_turing_8_rowscale",
                      "cigemmlt_ampere_32", "cigemmlt_ampere_8", "cigemmlt_ampere_8_rowscale",
-                     "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cget_last_error", "cget_abi_version"):
+                     "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cget_last_error", "cget_abi_version",
+                     "cgemm_4bit_inference_naive_nested_fp16", "cgemm_4bit_inference_naive_nested_bf16"):
             getattr(lib, name).restype = ct.c_int
 
     def __getattr__(self, item):

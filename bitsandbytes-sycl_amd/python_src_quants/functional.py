@@ -483,7 +483,6 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
         )
     Bshape = state.shape
     bout = Bshape[0]
-    absmax = _absmax_fp32(state)
     if out is None:
         if len(A.shape) == 3:
             out = torch.empty(size=(A.shape[0], A.shape[1], bout), dtype=A.dtype, device=A.device)
@@ -491,12 +490,28 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
             out = torch.empty(size=(A.shape[0], bout), dtype=A.dtype, device=A.device)
     m, n, k = Bshape[0], 1, Bshape[1]
     lda, ldc, ldb = Bshape[0], Bshape[0], (A.shape[-1] + 1) // 2
-    is_on_gpu([B, A, out, absmax, state.code])
     if B.dtype not in [torch.uint8, torch.bfloat16, torch.float16, torch.float32]:
         raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
     names = {torch.float16: "fp16", torch.bfloat16: "bf16", torch.float32: "fp32"}
     if A.dtype not in names:
         raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
+    if state.nested and A.dtype != torch.float32 and state.absmax.dtype == torch.uint8:
+        # compressed statistics decoded inside the GEMV kernel: one launch instead of
+        # dequantize_blockwise + gemv (ref:functional.py:1982-1984)
+        s2 = state.state2
+        offset = state.offset if torch.is_tensor(state.offset) else torch.tensor(float(state.offset))
+        offset = offset.to(device=A.device, dtype=torch.float32).reshape(1)
+        is_on_gpu([B, A, out, state.absmax, s2.absmax, s2.code, offset, state.code])
+        fn = getattr(lib, f"cgemm_4bit_inference_naive_nested_{names[A.dtype]}")
+        rc = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A), get_ptr(B), get_ptr(state.absmax),
+                get_ptr(s2.code), get_ptr(s2.absmax), get_ptr(offset), get_ptr(state.code), get_ptr(out),
+                ct.c_int32(lda), ct.c_int32(ldb), ct.c_int32(ldc), ct.c_int32(state.blocksize),
+                ct.c_int32(s2.blocksize))
+        if rc == 0:
+            post_call(prev_device)
+            return out
+    absmax = _absmax_fp32(state)
+    is_on_gpu([B, A, out, absmax, state.code])
     fn = getattr(lib, f"cgemm_4bit_inference_naive_{names[A.dtype]}")
     fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A), get_ptr(B), get_ptr(absmax), get_ptr(state.code),
        get_ptr(out), ct.c_int32(lda), ct.c_int32(ldb), ct.c_int32(ldc), ct.c_int32(state.blocksize))

@@ -69,6 +69,16 @@ void cgemm_4bit_inference_naive_bf16(int m, int n, int k, bnb_bf16* A, unsigned 
                                      bnb_bf16* out, int lda, int ldb, int ldc, int blocksize);   /* :411 */
 void cgemm_4bit_inference_naive_fp32(int m, int n, int k, float* A, unsigned char* B, float* absmax, float* datatype,
                                      float* out, int lda, int ldb, int ldc, int blocksize);      /* :414 */
+/* Additive: the same GEMV with compressed statistics (compress_statistics=True) decoded in-kernel,
+ * absmax[j] = code2[absmax_q[j]] * absmax2[j / blocksize2] + *offset (fp32), replacing the
+ * dequantize_blockwise launch of ref:python_src_quants/functional.py:1982-1984.  `offset` is a device
+ * pointer to one float.  Returns 0 when launched, 1 when the shape needs the two-step path. */
+int cgemm_4bit_inference_naive_nested_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, unsigned char* absmax_q,
+                                           float* code2, float* absmax2, float* offset, float* datatype, bnb_fp16* out,
+                                           int lda, int ldb, int ldc, int blocksize, int blocksize2);
+int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, unsigned char* absmax_q,
+                                           float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
+                                           int lda, int ldb, int ldc, int blocksize, int blocksize2);
 
 /* ---- 4-bit GEMM (any number of activation rows): ref:sycl/pythonInterface.cpp:377-378 (slot of the
  * broken kgemm_4bit_inference, re-implemented as a fused NF4 GEMM) ----

@@ -47,7 +47,8 @@ def test_gemv_golden(golden, dev):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("qt", ["nf4", "fp4"])
-@pytest.mark.parametrize("shape", [(11008, 4096), (4096, 11008), (1000, 192), (77, 64 * 33)])
+@pytest.mark.parametrize("shape", [(11008, 4096), (4096, 11008), (1000, 192), (77, 64 * 33), (300, 6144),
+                                   (37, 40960)])
 def test_gemv_functional(dev, dtype, qt, shape):
     F = _F()
     N, K = shape
@@ -63,6 +64,28 @@ def test_gemv_functional(dev, dtype, qt, shape):
         tol = {torch.bfloat16: 2e-2, torch.float16: 1e-2, torch.float32: 1e-4}[dtype]
         frac, err = _close(y.float().cpu().numpy()[0], exp, tol, tol)
         assert frac == 0.0, (nested, err)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(11008, 4096), (513, 6144), (4096, 11008), (64, 192)])
+def test_gemv_nested_fused_matches_two_step(dev, dtype, shape):
+    """The in-kernel decode of compressed statistics is bit-identical to dequantize_blockwise(absmax) +
+    offset (ref:functional.py:1982-1984) followed by the plain GEMV."""
+    F = _F()
+    N, K = shape
+    torch.manual_seed(7)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    x = torch.randn(1, K, device=dev, dtype=dtype)
+    fused = F.gemv_4bit(x, q.t(), state=st)
+    absmax = F._absmax_fp32(st)
+    ref_out = torch.empty_like(fused)
+    name = {torch.bfloat16: "bf16", torch.float16: "fp16"}[dtype]
+    getattr(F.lib, f"cgemm_4bit_inference_naive_{name}")(
+        ct.c_int32(N), ct.c_int32(1), ct.c_int32(K), F.get_ptr(x), F.get_ptr(q), F.get_ptr(absmax),
+        F.get_ptr(st.code), F.get_ptr(ref_out), ct.c_int32(N), ct.c_int32(K // 2), ct.c_int32(N), ct.c_int32(64))
+    torch.cuda.synchronize()
+    assert torch.equal(fused.view(torch.int16), ref_out.view(torch.int16))
 
 
 def test_gemv_generic_path(dev):

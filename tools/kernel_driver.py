@@ -33,6 +33,40 @@ def main():
         out = torch.empty(M, N, device=dev, dtype=torch.float16)
         fn = lambda: F.igemmlt_dequant(A, B, rs, cs, out=out)  # noqa: E731
         flops = 2.0 * M * N * K
+    elif what in ("gemv", "gemv16", "gemvn"):
+        # decode: M=1, N=11008, K=4096, 14 rotating weight copies (> MALL) replayed from one HIP graph
+        dt = torch.bfloat16 if what == "gemv" else torch.float16
+        n_out, k_in, copies = 11008, 4096, 14
+        ws = []
+        for _ in range(copies):
+            W = (torch.randn(n_out, k_in, device=dev) * 0.02).to(dt)
+            ws.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=(what == "gemvn")))
+        x = torch.randn(1, k_in, device=dev, dtype=dt)
+        out = torch.empty(1, n_out, device=dev, dtype=dt)
+        for q, st in ws:
+            F.gemv_4bit(x, q.t(), out=out, state=st)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for q, st in ws:
+                F.gemv_4bit(x, q.t(), out=out, state=st)
+        fn = g.replay
+        iters_per = copies
+        nbytes = n_out * k_in // 2 + n_out * k_in // 64 * 4 + k_in * 2 + n_out * 2
+        if what == "gemvn":   # 1-B codes + fp32 per 256 blocks + 1 KiB code map
+            nbytes = n_out * k_in // 2 + n_out * k_in // 64 + n_out * k_in // 64 // 256 * 4 + 1024 + k_in * 2 + n_out * 2
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / iters / iters_per * 1e-3
+        print(f"{what}: {t*1e6:.2f} us/call (graph), {nbytes / t / 1e9:.0f} GB/s")
+        return
     else:
         raise SystemExit(f"unknown {what}")
     for _ in range(3):
