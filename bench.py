@@ -79,50 +79,65 @@ def bench_int8(dev, m, n, k, iters=20):
             "forward_with_double_quant_us": t_fwd * 1e6}
 
 
-def bench_decode_gemv(dev, iters=60):
-    """Config 2: Linear4bit NF4 decode M=1, K=4096, N=11008, bf16, nested stats.  Rotates 14 weight copies
-    (>256 MiB) so the Infinity Cache cannot serve repeats; GB/s over the algorithmic bytes."""
+def _time_graph(calls, iters):
+    """Capture one pass over `calls` (distinct buffers each) into a HIP graph and time replays, so the
+    number is the kernels' back-to-back time rather than the Python launch rate."""
+    for c in calls:
+        c()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for c in calls:
+            c()
+    t = _time_loop(g.replay, iters, warmup=2)
+    return t / len(calls)
+
+
+def bench_decode_gemv(dev, iters=30):
+    """Config 2: Linear4bit NF4 decode M=1, K=4096, N=11008, bf16.  Both statistics formats: nested
+    (compress_statistics=True, the Linear4bit default; decoded inside the GEMV kernel) and plain fp32.
+    14 rotating weight copies (>256 MiB MALL) replayed from one HIP graph; GB/s over algorithmic bytes."""
     n_out, k_in = 11008, 4096
     copies = 14
     g = torch.Generator(device=dev).manual_seed(2)
-    ws = []
-    for _ in range(copies):
-        W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
-        q, st = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=False)
-        ws.append((q, st))
-        del W
     x = torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g)
     out = torch.empty(1, n_out, device=dev, dtype=torch.bfloat16)
-    idx = [0]
+    res = {"shape": [1, n_out, k_in]}
+    for nested in (True, False):
+        ws = []
+        for _ in range(copies):
+            W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+            ws.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=nested))
+            del W
+        calls = [(lambda q=q, st=st: F.gemv_4bit(x, q.t(), out=out, state=st)) for q, st in ws]
+        t = _time_graph(calls, iters)
+        if nested:   # packed + 1-B codes + fp32 per 256 blocks + 1 KiB map + offset + x + out
+            nbytes = n_out * k_in // 2 + n_out * k_in // BS + n_out * k_in // BS // 256 * 4 + 1024 + 4 + k_in * 2 + n_out * 2
+        else:
+            nbytes = n_out * k_in // 2 + n_out * k_in // BS * 4 + k_in * 2 + n_out * 2     # 25,392,640 B
+        res["nested" if nested else "plain"] = {"us": t * 1e6, "gbs": nbytes / t / 1e9,
+                                                "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS, "bytes": nbytes}
+        del ws
+    res["note"] = "14 rotating weight copies (~355 MB) defeat the 256 MB MALL; HIP-graph replay (kernel time)"
+    return res
 
-    def call():
-        q, st = ws[idx[0] % copies]
-        idx[0] += 1
-        F.gemv_4bit(x, q.t(), out=out, state=st)
-    t = _time_loop(call, iters, warmup=copies)
-    nbytes = n_out * k_in // 2 + n_out * k_in // BS * 4 + k_in * 2 + n_out * 2   # 25,392,640 B
-    return {"shape": [1, n_out, k_in], "us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS,
-            "bytes": nbytes, "note": "non-nested absmax; 14 rotating weight copies (~355 MB) defeat the 256 MB MALL"}
 
-
-def bench_dequant_config1(dev, iters=40):
+def bench_dequant_config1(dev, iters=30):
     """Config 1 on the GPU: dequantize_blockwise NF4 of a 4096x4096 weight, bs=64 -> bf16 (HBM-bound)."""
     g = torch.Generator(device=dev).manual_seed(0)
-    copies = 8
+    copies = 30       # 30 x 9.4 MB of packed input > 256 MB MALL
     qs = []
     for _ in range(copies):
         W = torch.randn(4096, 4096, device=dev, generator=g)
         qs.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4"))
-    out = torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16)
-    idx = [0]
+    outs = [torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16) for _ in range(2)]
 
-    def call():
-        q, st = qs[idx[0] % copies]
-        idx[0] += 1
-        F.lib.cdequantize_blockwise_bf16_nf4(None, F.get_ptr(q), F.get_ptr(st.absmax), F.get_ptr(out), ct.c_int(BS),
-                                              ct.c_int(4096 * 4096))
-    F.pre_call(dev)
-    t = _time_loop(call, iters, warmup=copies)
+    def call(q, st, o):
+        F.pre_call(dev)      # binds the library to the current (capturing) stream
+        F.lib.cdequantize_blockwise_bf16_nf4(None, F.get_ptr(q), F.get_ptr(st.absmax), F.get_ptr(o), ct.c_int(BS),
+                                             ct.c_int(4096 * 4096))
+    calls = [(lambda q=q, st=st, o=outs[i % 2]: call(q, st, o)) for i, (q, st) in enumerate(qs)]
+    t = _time_graph(calls, iters)
     nbytes = 42_991_616
     return {"us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS, "bytes": nbytes}
 
@@ -167,6 +182,13 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
                       f"NF4 bs=64 unpacked ({t_deq:.3f}s, {n_el * 9 / t_deq / 1e9:.2f} GB/s) + torch CPU fp32 "
                       f"F.linear on {rows} of the {M} rows ({t_mm:.3f}s, {threads} threads); median rep",
             "dequant_cpu_gbs": n_el * 9 / t_deq / 1e9}
+
+
+def gemm_kernel_name(m, n):
+    """Which tile kernel gemm_4bit dispatches to (gemm4bit.hip: 256x256 when both sides >= 256 and the
+    256-tile grid still has >= 128 workgroups)."""
+    tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
+    return "k_gemm_4bit_256<bf16>" if (m >= 256 and n >= 256 and tiles256 >= 128) else "k_gemm_4bit<bf16>"
 
 
 def load_pmc_traffic():
@@ -263,7 +285,7 @@ def main():
     if rank == 0:
         pmc = load_pmc_traffic()
         traffic = None
-        if pmc and pmc.get("kernel_prefix") and pmc.get("shape") == [M, shard, K]:
+        if pmc and pmc.get("kernel") == gemm_kernel_name(M, shard) and pmc.get("shape") == [M, shard, K]:
             traffic = pmc.get("hbm_bytes_per_launch")
         line = {
             "metric": "NF4 matmul TFLOPS + INT8 igemmlt TOPS @ 4096x4096x11008, 1/2/4/8 GPU",
@@ -284,7 +306,7 @@ def main():
                        "parallelism": f"column-shard x{world} + RCCL all_gather" if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                         "kernel": "k_gemm_4bit<bf16>", "kernel_us": round(kern_s * 1e6, 2),
+                         "kernel": gemm_kernel_name(M, shard), "kernel_us": round(kern_s * 1e6, 2),
                          "flops_per_launch": shard_flops},
             "cpu_baseline": cpu,
         }
