@@ -230,6 +230,57 @@ k_dequantize_blockwise(const float* __restrict__ code, const uint8_t* __restrict
   }
 }
 
+template <typename T> struct Pack2;
+template <> struct Pack2<bf16_t> {
+  __device__ static __forceinline__ uint32_t pk(float a, float b) { return pack_bf16x2(a, b); }
+};
+template <> struct Pack2<fp16_t> {
+  __device__ static __forceinline__ uint32_t pk(float a, float b) { return Store<fp16_t>::pk(a, b); }
+};
+
+// 4-bit -> bf16/fp16 streaming dequantize (n % 8 == 0, 4-B aligned input, 16-B aligned output).
+// Lane l of wave w owns packed dwords base + 64*(P*w + j) + l, j < P: every load instruction reads
+// 256 contiguous bytes and every store instruction writes 1 KiB contiguous (8 outputs per lane).
+// All P loads (+ their absmax) are issued before any is consumed.  Values are fp32 code*absmax,
+// then one RNE cast -- identical to k_dequantize_blockwise.
+template <typename T, int DT, int P>
+__global__ void __launch_bounds__(256)
+k_dequantize_4bit_stream(const uint8_t* __restrict__ A, const float* __restrict__ absmax, T* __restrict__ out,
+                         int bs_shift, long long ndw) {
+  __shared__ float2 s_pair[256];
+  s_pair[threadIdx.x] = make_float2(code4_value<DT>(threadIdx.x >> 4), code4_value<DT>(threadIdx.x & 15));
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t* Aw = reinterpret_cast<const uint32_t*>(A);
+  for (long long base = (long long)blockIdx.x * 256 * P; base < ndw; base += (long long)gridDim.x * 256 * P) {
+    uint32_t w[P];
+    float am[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const long long d = min(base + 64LL * (P * wave + j) + lane, ndw - 1);
+      w[j] = __builtin_nontemporal_load(Aw + d);
+      am[j] = absmax[(8 * d) >> bs_shift];
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const long long d = base + 64LL * (P * wave + j) + lane;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 p = s_pair[(w[j] >> (8 * i)) & 0xFF];
+        v[2 * i] = __fmul_rn(p.x, am[j]);
+        v[2 * i + 1] = __fmul_rn(p.y, am[j]);
+      }
+      if (d < ndw) {
+        uint4 o;
+        o.x = Pack2<T>::pk(v[0], v[1]); o.y = Pack2<T>::pk(v[2], v[3]);
+        o.z = Pack2<T>::pk(v[4], v[5]); o.w = Pack2<T>::pk(v[6], v[7]);
+        reinterpret_cast<uint4*>(out)[d] = o;
+      }
+    }
+  }
+}
+
 // ============================================================================ CPU-path semantics
 // The reference's host-pointer functions (cpu_ops.cpp).  Here they are executed on the GPU:
 // host buffers are staged into HBM, processed by the kernels below, and copied back.
@@ -322,6 +373,21 @@ template <typename T, int DT>
 void dequantize_blockwise(const float* code, const uint8_t* A, const float* absmax, T* out, int blocksize, long long n) {
   if (n <= 0) return;
   if (blocksize < 64 || (blocksize & (blocksize - 1))) { set_error(1, "dequantize_blockwise: unsupported blocksize"); return; }
+  if constexpr (DT != GENERAL8BIT && sizeof(T) == 2) {
+    if (n % 8 == 0 && ((uintptr_t)A & 3) == 0 && aligned16(out)) {
+#ifndef BNB_DQ_P
+#define BNB_DQ_P 8
+#endif
+      constexpr int P = BNB_DQ_P;
+      const long long ndw = n / 8;
+      const long long wgs = (ndw + 256 * P - 1) / (256 * P);
+      const int grid = (int)(wgs < 65536 ? wgs : 65536);
+      hipLaunchKernelGGL((k_dequantize_4bit_stream<T, DT, P>), dim3(grid), dim3(256), 0, current_stream(), A, absmax,
+                         out, __builtin_ctz(blocksize), ndw);
+      BNB_LAUNCH_CHECK("dequantize_blockwise");
+      return;
+    }
+  }
   const long long nbytes = (DT == GENERAL8BIT) ? n : (n + 1) / 2;
   const int grid = stream_grid((nbytes + 15) / 16, 256);
   const bool vec = aligned16(A) && aligned16(out);

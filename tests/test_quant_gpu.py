@@ -74,7 +74,7 @@ def test_random_sizes_bit_exact(dev, qtype, bs, dtype):
     F = _F()
     code = create_dynamic_map()
     rng = np.random.default_rng(bs * 7 + len(qtype))
-    for n in (bs * 37 + 3, bs - 1, 2 * bs, 1, 131071):
+    for n in (bs * 37 + 3, bs - 1, 2 * bs, 1, 131071, 8 * 100003):
         x = (rng.standard_normal(n) * rng.uniform(0.1, 10)).astype(np.float32)
         if n > 3:
             x[rng.integers(0, n, 3)] = np.nan
@@ -84,7 +84,7 @@ def test_random_sizes_bit_exact(dev, qtype, bs, dtype):
         absmax, q = _run_quant(F, dev, a, dtype, qtype, bs, code)
         assert same_bits(absmax, ea), (n, "absmax")
         assert same_bits(q, eq), (n, "codes", np.flatnonzero(q != eq)[:8])
-        for od in ("bf16", "fp32"):
+        for od in ("bf16", "fp16", "fp32"):
             y = _run_dequant(F, dev, eq, ea, n, qtype, bs, od, code)
             assert same_bits(y, ref.dequantize_blockwise(eq, ea, bs, n, qtype, od, code=code)), (n, od)
 

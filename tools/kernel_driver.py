@@ -67,6 +67,35 @@ def main():
         t = s.elapsed_time(e) / iters / iters_per * 1e-3
         print(f"{what}: {t*1e6:.2f} us/call (graph), {nbytes / t / 1e9:.0f} GB/s")
         return
+    elif what == "dequant":
+        # config 1 on the GPU: NF4 4096x4096 bs=64 -> bf16, 30 rotating copies, one HIP graph
+        copies = 30
+        qs = [F.quantize_4bit(torch.randn(4096, 4096, device=dev), blocksize=64, quant_type="nf4") for _ in range(copies)]
+        outs = [torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+
+        def call(q, st, o):
+            F.pre_call(dev)
+            F.lib.cdequantize_blockwise_bf16_nf4(None, F.get_ptr(q), F.get_ptr(st.absmax), F.get_ptr(o),
+                                                 ct.c_int(64), ct.c_int(4096 * 4096))
+        for i, (q, st) in enumerate(qs):
+            call(q, st, outs[i % 2])
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i, (q, st) in enumerate(qs):
+                call(q, st, outs[i % 2])
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            g.replay()
+        e.record()
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / iters / copies * 1e-3
+        print(f"dequant: {t*1e6:.2f} us/call (graph), {42991616 / t / 1e9:.0f} GB/s")
+        return
     else:
         raise SystemExit(f"unknown {what}")
     for _ in range(3):
