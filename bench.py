@@ -209,6 +209,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-extras", action="store_true", help="skip int8/decode/config-1/cpu legs")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +245,13 @@ def main():
         if world > 1:
             dist.all_gather_into_tensor(gathered, Y)
 
+    # clock ramp: MI355X takes ~0.1-0.3 s of sustained MFMA load to reach its steady clock; run the
+    # step untimed for --prewarm-ms before the W counted warmup steps (the timed region is unchanged)
+    # (GEMM only: a time-based loop must not contain a collective, ranks could disagree on its count)
+    t_end = time.perf_counter() + args.prewarm_ms / 1e3
+    while time.perf_counter() < t_end:
+        F.gemm_4bit(X, q, st, out=Y, absmax=F._absmax_fp32(st))
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

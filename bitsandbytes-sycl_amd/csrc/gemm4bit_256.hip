@@ -2,19 +2,22 @@
 // see gemm4bit.hip for the ABI / semantics; ref:sycl/pythonInterface.cpp:377-378, kernel_gemm.cpp:1015).
 //
 // Geometry: 512 threads = 8 waves (2 along tokens x 4 along out-features), 128 x 64 outputs per wave
-// (8 x 4 tiles of v_mfma_f32_16x16x32), BK = 64, one workgroup per CU (148 KiB LDS).
+// (4 x 2 tiles of v_mfma_f32_32x32x16), BK = 64, one workgroup per CU (148 KiB LDS).  The 32x32x16
+// MFMA holds the SIMD's issue for 8 of its 32 cycles, so the dequantisation and DMA issue fit beside it.
 //
 // Every operand arrives by LDS-DMA (global_load_lds), so no VGPR-destination load is ever in flight
 // in the k-loop (hipcc otherwise drains the prefetch early, cdna_hip_programming.md §5):
-//   Xs[2]  activations   2 x 32 KiB  [256][64] T, XOR-swizzled through the source address
+//   Xs[2]  activations   2 x 32 KiB  [256][64] T, 16-B slots XOR-swizzled by (row >> 1) & 7
 //   Ws[2]  weights (T)   2 x 32 KiB  same layout, written by the in-kernel dequantisation
 //   Wp[2]  packed 4-bit  2 x  8 KiB  [256 rows][2 halves][16 B], lane-linear
 //   Am[2]  absmax        2 x  1 KiB  one fp32 per weight row and k-step (bs >= 64)
 //   LUT                      2 KiB   byte -> {code[hi], code[lo]}
-// k-step t (one barrier): DMA X(t+1), W(t+2) packed, absmax(t+2); 64 MFMAs per wave on stage t,
-// interleaved with the dequantisation of W(t+1) (Wp -> LUT -> *absmax -> one RNE cast -> Ws);
-// vmcnt(0) + barrier.  The body is branch-free (prefetch indices are clamped) so the scheduler can
-// interleave the dequant VALU/LDS work between the MFMAs.
+// The swizzle makes the 32-row fragment reads (ds_read_b128 lane groups) and the dequant stores
+// (8 consecutive lanes -> rows 2i+p, distinct XOR keys) conflict-free.
+// k-step t (one barrier): the four k16 sub-steps each issue one X(t+1) DMA piece (W(t+2) and its
+// absmax ride with the first), run 8 MFMAs on stage t, and dequantise one quarter of this thread's
+// 16 packed bytes of W(t+1) (LUT -> *absmax -> one RNE cast -> Ws) -- the reference's dequantised
+// values; vmcnt(0) + barrier.
 #include "gemm_common.hpp"
 
 namespace bnb {
@@ -36,32 +39,22 @@ static_assert(8 * 128 * Q_EPI_STRIDE <= Q_OFF_L, "epilogue staging must not over
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
-// one packed byte -> {T(code[hi]*am), T(code[lo]*am)} as a dword: ds_read_b64 of the pair table,
-// v_pk_mul_f32 by the broadcast absmax, one v_cvt_pk (RNE) -- the reference's dequantised values.
-template <typename T> __device__ __forceinline__ uint32_t deq_byte(const f32x2_t* lut, uint32_t byte, f32x2_t am2);
-template <> __device__ __forceinline__ uint32_t deq_byte<bf16_t>(const f32x2_t* lut, uint32_t byte, f32x2_t am2) {
-  const f32x2_t p = lut[byte] * am2;
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2_t));
-}
-template <> __device__ __forceinline__ uint32_t deq_byte<fp16_t>(const f32x2_t* lut, uint32_t byte, f32x2_t am2) {
-  const f32x2_t p = lut[byte] * am2;
-  return Mfma<fp16_t>::pack2(p.x, p.y);
+__device__ __forceinline__ int swz2(int r, int s) { return r * 128 + ((s ^ ((r >> 1) & 7)) << 4); }
+
+// scalar v_mul_f32 (hipcc would SLP-pack the pair into v_pk_mul_f32, which costs ~4x the issue
+// slots beside MFMAs on gfx950)
+__device__ __forceinline__ float mul_f32(float a, float b) {
+  float r;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
-template <typename T>
-__device__ __forceinline__ void dequant_slot_pair(uint8_t* ws, const float2* lut, uint32_t w0, uint32_t w1, float am,
-                                                  int row, int slot0) {
-  const uint32_t w[2] = {w0, w1};
-  const f32x2_t am2 = {am, am};
-  const f32x2_t* lut2 = reinterpret_cast<const f32x2_t*>(lut);
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    uint32_t pk[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) pk[j] = deq_byte<T>(lut2, (w[s] >> (8 * j)) & 0xFF, am2);
-    *reinterpret_cast<uint4*>(ws + swz(row, slot0 + s)) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-  }
+// {T(lo), T(hi)} with one RNE cast each (v_cvt_pk_bf16_f32 for bf16)
+template <typename T> __device__ __forceinline__ uint32_t cvt2(float lo, float hi);
+template <> __device__ __forceinline__ uint32_t cvt2<bf16_t>(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
+template <> __device__ __forceinline__ uint32_t cvt2<fp16_t>(float lo, float hi) { return Mfma<fp16_t>::pack2(lo, hi); }
 
 template <typename T>
 __global__ void __launch_bounds__(Q_THREADS, 1)
@@ -90,10 +83,9 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = 8 * (4 * wave + i) + (lane >> 3);
-    xsrc[i] = A + (long long)min(m0 + row, M - 1) * lda + 8 * ((lane & 7) ^ (row & 7));
+    xsrc[i] = A + (long long)min(m0 + row, M - 1) * lda + 8 * ((lane & 7) ^ ((row >> 1) & 7));
   }
-  const int prow = tid >> 1, phalf = tid & 1;                       // this lane's packed 16 B
-  const uint8_t* psrc = B + (long long)min(n0 + prow, N - 1) * ldb + 16 * phalf;
+  const uint8_t* psrc = B + (long long)min(n0 + (tid >> 1), N - 1) * ldb + 16 * (tid & 1);   // lane-linear
   // absmax DMA: one row per lane; waves 4-7 repeat waves 0-3 into the stage's spare copy (branch-free)
   const int arow = 64 * (wave & 3) + lane;
   const int bs_shift = __builtin_ctz(blocksize);                    // blocksize: power of two >= 64
@@ -104,54 +96,85 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
     glds16(psrc + (long long)kt * (Q_BK / 2), smem + Q_OFF_P + buf * Q_PT + wave * 1024);
     glds4(absmax + ((abase + (long long)kt * Q_BK) >> bs_shift), smem + Q_OFF_A + buf * Q_AT + wave * 256);
   };
-  auto dma_x = [&](int kt, int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      glds16(xsrc[i] + (long long)kt * Q_BK, smem + Q_OFF_X + buf * Q_XT + (4 * wave + i) * 1024);
+  auto dma_x_piece = [&](int kt, int buf, int i) {
+    glds16(xsrc[i] + (long long)kt * Q_BK, smem + Q_OFF_X + buf * Q_XT + (4 * wave + i) * 1024);
   };
-  auto dequant_half = [&](int buf_src, int buf_dst, int h) {       // h = 0/1: first/second 8 packed bytes
-    const uint8_t* p = smem + Q_OFF_P + buf_src * Q_PT + 16 * tid;
-    const uint2 w = *reinterpret_cast<const uint2*>(p + 8 * h);
-    const float am = *reinterpret_cast<const float*>(smem + Q_OFF_A + buf_src * Q_AT + 4 * prow);
-    dequant_slot_pair<T>(smem + Q_OFF_W + buf_dst * Q_WT, lut, w.x, w.y, am, prow, 4 * phalf + 2 * h);
+
+  // ---- dequant role: this thread owns 16 packed bytes (32 k) of one W row; 8 consecutive lanes take
+  // rows 2i+p so their 16-B stores land on distinct swizzle keys
+  const int g = lane & 31;
+  const int drow = 16 * (tid >> 5) + 2 * (g & 7) + ((g >> 3) & 1);
+  const int dhalf = (g >> 4) & 1;
+  auto lut_reads = [&](uint32_t word, float2 (&c)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = lut[(word >> (8 * j)) & 0xFF];
+  };
+  auto finish = [&](const float2 (&c)[4], float am, uint8_t* ws, int q) {   // 4 bytes -> one 16-B slot
+    uint32_t pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pk[j] = cvt2<T>(mul_f32(c[j].x, am), mul_f32(c[j].y, am));
+    *reinterpret_cast<uint4*>(ws + swz2(drow, 4 * dhalf + q)) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  };
+  auto packed_of = [&](int buf, uint32_t (&w4)[4], float& am) {
+    const uint4 pw = *reinterpret_cast<const uint4*>(smem + Q_OFF_P + buf * Q_PT + drow * 32 + 16 * dhalf);
+    w4[0] = pw.x; w4[1] = pw.y; w4[2] = pw.z; w4[3] = pw.w;
+    am = *reinterpret_cast<const float*>(smem + Q_OFF_A + buf * Q_AT + 4 * drow);
   };
 
   const int wm = wave >> 2, wn = wave & 3;
-  f32x4_t acc[8][4];
+  f32x16_t acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // ---- prologue: X(0), W(0), W(1) in flight; dequantise W(0) into Ws[0]
-  dma_x(0, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_x_piece(0, 0, i);
   dma_w(0, 0);
   dma_w(min(1, nk - 1), 1);
   wait_vmcnt0();
   __syncthreads();
-  dequant_half(0, 0, 0);
-  dequant_half(0, 0, 1);
+  {
+    uint32_t w4[4];
+    float am;
+    packed_of(0, w4, am);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float2 c[4];
+      lut_reads(w4[q], c);
+      finish(c, am, smem + Q_OFF_W, q);
+    }
+  }
   __syncthreads();
 
   for (int t = 0; t < nk; ++t) {
     const int s = t & 1;
-    dma_x(min(t + 1, nk - 1), s ^ 1);
-    dma_w(min(t + 2, nk - 1), s);
     const uint8_t* xs = smem + Q_OFF_X + s * Q_XT;
     const uint8_t* ws = smem + Q_OFF_W + s * Q_WT;
+    uint8_t* wsn = smem + Q_OFF_W + (s ^ 1) * Q_WT;
+    uint32_t w4[4];
+    float am;
+    packed_of(s ^ 1, w4, am);                                      // W(t+1), landed during step t-1
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int slot = 4 * ks + (lane >> 4);
-      uint4 b[4];
+    for (int ks = 0; ks < 4; ++ks) {
+      dma_x_piece(min(t + 1, nk - 1), s ^ 1, ks);
+      if (ks == 0) dma_w(min(t + 2, nk - 1), s);
+      const int slot = 2 * ks + (lane >> 5);
+      uint4 a[4], b[2];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(ws + swz(64 * wn + 16 * j + (lane & 15), slot));
+      for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const uint4*>(ws + swz2(64 * wn + 32 * j + (lane & 31), slot));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint4 a = *reinterpret_cast<const uint4*>(xs + swz(128 * wm + 16 * i + (lane & 15), slot));
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const uint4*>(xs + swz2(128 * wm + 32 * i + (lane & 31), slot));
+      float2 c[4];
+      lut_reads(w4[ks], c);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = Mfma<T>::mma(a, b[j], acc[i][j]);
-      }
-      dequant_half(s ^ 1, s ^ 1, ks);   // W(t+1): Wp[(t+1)&1] -> Ws[(t+1)&1]
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = Mfma32<T>::mma(a[i], b[j], acc[i][j]);
+      finish(c, am, wsn, ks);
     }
     wait_vmcnt0();
     __syncthreads();
@@ -160,12 +183,12 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
   // ---- epilogue: acc -> LDS (per-wave [128][64] T, 136-B rows) -> 16-B coalesced stores
   uint8_t* ep = smem + wave * (128 * Q_EPI_STRIDE);
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * i + 4 * (lane >> 4) + r, col = 16 * j + (lane & 15);
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * i + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3), col = 32 * j + (lane & 31);
         *reinterpret_cast<T*>(ep + row * Q_EPI_STRIDE + 2 * col) = Io<T>::from_f32(acc[i][j][r]);
       }
   __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the wave reads back only its own region

@@ -18,6 +18,22 @@ template <> struct Mfma<bf16_t> {
   }
   __device__ static __forceinline__ uint32_t pack2(float lo, float hi) { return pack_bf16x2(lo, hi); }
 };
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+// 32x32x16 (gfx950): lane l holds A[row l&31][k 8(l>>5)..+8] and B[k 8(l>>5)..+8][col l&31];
+// D[r]: row 8(r>>2) + 4(l>>5) + (r&3), col l&31.  An MFMA holds the SIMD's vector issue for 8 of
+// its 32 cycles (vs 8 of 16 for 16x16x32), leaving 3x the issue slots for the in-loop dequant.
+template <typename T> struct Mfma32;
+template <> struct Mfma32<bf16_t> {
+  __device__ static __forceinline__ f32x16_t mma(const uint4& a, const uint4& b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma32<fp16_t> {
+  __device__ static __forceinline__ f32x16_t mma(const uint4& a, const uint4& b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  }
+};
+
 template <> struct Mfma<fp16_t> {
   __device__ static __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);

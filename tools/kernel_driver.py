@@ -96,9 +96,19 @@ def main():
         t = s.elapsed_time(e) / iters / copies * 1e-3
         print(f"dequant: {t*1e6:.2f} us/call (graph), {42991616 / t / 1e9:.0f} GB/s")
         return
+    elif what == "nf4gemm_rand":   # uniform random packed bytes / absmax 0.01 (the lab's data)
+        M, N, K = 4096, 4096, 11008
+        X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
+        q.copy_(torch.randint(0, 256, q.shape, device=dev, dtype=torch.uint8))
+        st.absmax.fill_(0.01)
+        Y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        fn = lambda: F.gemm_4bit(X, q, st, out=Y, absmax=st.absmax)  # noqa: E731
+        flops = 2.0 * M * N * K
     else:
         raise SystemExit(f"unknown {what}")
-    for _ in range(3):
+    for _ in range(int(os.environ.get("KD_WARMUP", "3"))):
         fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
