@@ -623,6 +623,163 @@ k_lab32c(int N, int M, int K, const bf16_t* __restrict__ A, const uint8_t* __res
     *reinterpret_cast<uint4*>(out + (long long)grow * ldc + gcol) = make_uint4(lo.x, lo.y, hi.x, hi.y);
   }
 }
+
+// ---- v3: X ring of 3 stages (DMA two steps ahead), single W buffer with a mid-step barrier,
+// B fragments of the whole step read up front
+constexpr int V3_OFF_X = 0;                         // 3 x 32 KiB
+constexpr int V3_OFF_W = 3 * Q_XT;                  // 32 KiB
+constexpr int V3_OFF_P = V3_OFF_W + Q_WT;           // 2 x 8 KiB
+constexpr int V3_OFF_A = V3_OFF_P + 2 * Q_PT;       // 2 x 1 KiB
+constexpr int V3_OFF_L = V3_OFF_A + 2 * 1024;       // 2 KiB
+constexpr int V3_LDS = V3_OFF_L + 2048;
+template <int FL>
+__global__ void __launch_bounds__(Q_THREADS, 1)
+k_lab3(int N, int M, int K, const bf16_t* __restrict__ A, const uint8_t* __restrict__ B,
+       const float* __restrict__ absmax, const float* __restrict__ datatype, bf16_t* __restrict__ out,
+       int lda, int ldb, int ldc, int blocksize) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  float2* lut = reinterpret_cast<float2*>(smem + V3_OFF_L);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < 256) lut[tid] = make_float2(datatype[tid >> 4], datatype[tid & 15]);
+  const int tilesN = (N + Q_BN - 1) / Q_BN, tilesM = (M + Q_BM - 1) / Q_BM;
+  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  constexpr int GROUP = 4;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * Q_BM, n0 = tn * Q_BN;
+  const bf16_t* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wave + i) + (lane >> 3);
+    xsrc[i] = A + (long long)min(m0 + row, M - 1) * lda + 8 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  const uint8_t* psrc = B + (long long)min(n0 + (tid >> 1), N - 1) * ldb + 16 * (tid & 1);
+  const int arow = 64 * (wave & 3) + lane;
+  const int bs_shift = __builtin_ctz(blocksize);
+  const long long abase = 2LL * ldb * min(n0 + arow, N - 1);
+  const int nk = K / Q_BK;
+  auto dma_w = [&](int kt, int buf) {
+    glds16(psrc + (long long)kt * (Q_BK / 2), smem + V3_OFF_P + buf * Q_PT + wave * 1024);
+    if (wave < 4) glds4(absmax + ((abase + (long long)kt * Q_BK) >> bs_shift), smem + V3_OFF_A + buf * 1024 + wave * 256);
+  };
+  auto dma_x_piece = [&](int kt, int buf, int i) {
+    glds16(xsrc[i] + (long long)kt * Q_BK, smem + V3_OFF_X + buf * Q_XT + (4 * wave + i) * 1024);
+  };
+  const int g = lane & 31;
+  const int drow = 16 * (tid >> 5) + 2 * (g & 7) + ((g >> 3) & 1);
+  const int dhalf = (g >> 4) & 1;
+  auto lut_reads = [&](uint32_t word, float2 (&c)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c[j] = lut[(word >> (8 * j)) & 0xFF];
+  };
+  uint8_t* wbuf = smem + V3_OFF_W;
+  auto finish = [&](const float2 (&c)[4], float am, int q) {
+    uint32_t pk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = mul_nopk(c[j].x, am), hi = mul_nopk(c[j].y, am);
+      pk[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+    }
+    *reinterpret_cast<uint4*>(wbuf + swz2(drow, 4 * dhalf + q)) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  };
+  auto packed_of = [&](int buf, uint32_t (&w4)[4], float& am) {
+    const uint4 pw = *reinterpret_cast<const uint4*>(smem + V3_OFF_P + buf * Q_PT + drow * 32 + 16 * dhalf);
+    w4[0] = pw.x; w4[1] = pw.y; w4[2] = pw.z; w4[3] = pw.w;
+    am = *reinterpret_cast<const float*>(smem + V3_OFF_A + buf * 1024 + 4 * drow);
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  f32x16_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // prologue: X(0), X(1), W(0), W(1); W(0) dequantised
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_x_piece(0, 0, i);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_x_piece(min(1, nk - 1), 1, i);
+  dma_w(0, 0);
+  dma_w(min(1, nk - 1), 1);
+  wait_vmcnt0();
+  __syncthreads();
+  {
+    uint32_t w4[4];
+    float am;
+    packed_of(0, w4, am);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float2 c[4];
+      lut_reads(w4[q], c);
+      finish(c, am, q);
+    }
+  }
+  __syncthreads();
+  int sx = 0;                                   // X stage of step t (t % 3)
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* xs = smem + V3_OFF_X + sx * Q_XT;
+    const int sx2 = sx == 0 ? 2 : sx - 1;       // (t + 2) % 3
+    uint4 b[4][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        b[ks][j] = *reinterpret_cast<const uint4*>(wbuf + swz2(64 * wn + 32 * j + (lane & 31), 2 * ks + (lane >> 5)));
+    uint32_t w4[4];
+    float am;
+    packed_of((t + 1) & 1, w4, am);
+    __builtin_amdgcn_s_waitcnt(0xC07F);         // lgkmcnt(0): every B fragment of W(t) is in registers
+    __builtin_amdgcn_s_barrier();               // ... in every wave, so W(t+1) may overwrite the buffer
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks == 0) dma_w(min(t + 2, nk - 1), t & 1);
+      dma_x_piece(min(t + 2, nk - 1), sx2, ks);
+      const int slot = 2 * ks + (lane >> 5);
+      uint4 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const uint4*>(xs + swz2(128 * wm + 32 * i + (lane & 31), slot));
+      float2 c[4];
+      if (!(FL & 2)) lut_reads(w4[ks], c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a[i]),
+                                                              __builtin_bit_cast(bf16x8_t, b[ks][j]), acc[i][j], 0, 0, 0);
+      if (!(FL & 2)) finish(c, am, ks);
+    }
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // X(t+2) may stay in flight; W(t+2), X(t+1) landed
+    __syncthreads();
+    sx = sx == 2 ? 0 : sx + 1;
+  }
+  uint8_t* ep = smem + wave * (128 * Q_EPI_STRIDE);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * i + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3), col = 32 * j + (lane & 31);
+        *reinterpret_cast<bf16_t*>(ep + row * Q_EPI_STRIDE + 2 * col) = Io<bf16_t>::from_f32(acc[i][j][r]);
+      }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = lane + 64 * it;
+    const int row = id >> 3, c8 = id & 7;
+    const int grow = grow0 + row, gcol = gcol0 + 8 * c8;
+    if (grow >= M) continue;
+    const uint2 lo = *reinterpret_cast<const uint2*>(ep + row * Q_EPI_STRIDE + 16 * c8);
+    const uint2 hi = *reinterpret_cast<const uint2*>(ep + row * Q_EPI_STRIDE + 16 * c8 + 8);
+    *reinterpret_cast<uint4*>(out + (long long)grow * ldc + gcol) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
 }
 using namespace bnb;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -644,36 +801,23 @@ int main() {
   float hc[16]; for (int i = 0; i < 16; ++i) hc[i] = (i - 7.5f) / 8; CK(hipMemcpy(code, hc, 64, hipMemcpyHostToDevice));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int tiles = (M / 256) * (N / 256);
-  auto run = [&](const char* name, auto kern) {
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
+  auto run = [&](const char* name, auto kern, size_t dyn = 0) {
+    if (dyn) CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), dyn, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
     const int R = 20;
-    for (int i = 0; i < R; ++i) hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
+    for (int i = 0; i < R; ++i) hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), dyn, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / R;
     printf("%-28s %8.1f us  %7.1f TFLOP/s\n", name, us, 2.0 * M * N * K / us / 1e6);
   };
-  run("full", k_lab<bf16_t, 0>);
-  run("no-dma", k_lab<bf16_t, 1>);
-  run("no-dequant", k_lab<bf16_t, 2>);
-  run("no-dma,no-dequant", k_lab<bf16_t, 3>);
-  run("no-dma,no-deq,no-barrier", k_lab<bf16_t, 7>);
-  run("32x32 full", k_lab32<0>);
-  run("32x32 no-dma", k_lab32<1>);
-  run("32x32 no-dequant", k_lab32<2>);
-  run("32x32 no-dma,no-dequant", k_lab32<3>);
-  run("32x32 setprio", k_lab32<8>);
-  run("32x32 spread-dma", k_lab32<16>);
-  run("32x32 setprio+spread", k_lab32<24>);
+  for (int rep = 0; rep < 2; ++rep) {
   run("32b full", k_lab32b<0>);
-  run("32b setprio", k_lab32b<8>);
-  run("32b no-dequant", k_lab32b<2>);
   run("32b no-dma", k_lab32b<1>);
-  run("32c full", k_lab32c<0>);
-  run("32c setprio", k_lab32c<8>);
-  run("32c no-dequant", k_lab32c<2>);
-  run("32c no-dma", k_lab32c<1>);
+  run("v3 full", k_lab3<0>, V3_LDS);
+  run("v3 no-dequant", k_lab3<2>, V3_LDS);
+  }
   return 0;
 }
