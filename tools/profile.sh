@@ -10,5 +10,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OU
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/fetch -- python3 bench.py --no-extras --no-cpu --steps 3 --warmup 1 > /dev/null 2> $OUT/fetch.err || exit 2
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/write -- python3 bench.py --no-extras --no-cpu --steps 3 --warmup 1 > /dev/null 2> $OUT/write.err || exit 3
 python3 tools/pmc_traffic.py $OUT/fetch $OUT/write "k_gemm_4bit_256" $OUT/pmc_traffic.json 4096 4096 11008 "k_gemm_4bit_256<bf16>" || exit 4
-find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/${TAG}_kernel_stats.csv ;
+find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/${TAG}_kernel_stats.csv \;
 echo "profile done"
