@@ -23,6 +23,8 @@
 // XCD-aware tile order keeps the tiles that share activation panels on one XCD's L2.
 #include "gemm_common.hpp"
 
+#include <algorithm>
+
 namespace bnb {
 
 constexpr int G_BM = 128, G_BN = 128, G_BK = 64, G_THREADS = 256;
@@ -157,22 +159,42 @@ k_gemm_4bit(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restr
 
 int g_tile_override = 0;
 
+// Split-K factor for the 256-tile kernel: enough workgroups to cover the 256 CUs when the output has
+// fewer than ~200 256x256 tiles (narrow column shards, e.g. N/8 = 512 features at M = 4096), with at
+// least 8 k-tiles per split.  Needs a caller-supplied fp32 workspace of ksplit * m * n floats.
+static int splitk_factor(int m, int n, int k) {
+  if (m < 256 || n < 256) return 1;
+  const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
+  if (tiles >= 200) return 1;
+  int ks = (int)((256 + tiles / 2) / tiles);
+  ks = std::min(ks, std::max(1, (k / G_BK) / 8));
+  return std::max(1, std::min(ks, 16));
+}
+
+long long gemm_4bit_workspace_bytes(int m, int n, int k) {
+  const int ks = splitk_factor(m, n, k);
+  return ks > 1 ? (long long)ks * m * n * (long long)sizeof(float) : 0;
+}
+
 template <typename T>
 void gemm_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype, T* out,
-               int lda, int ldb, int ldc, int blocksize) {
+               int lda, int ldb, int ldc, int blocksize, float* ws = nullptr, long long ws_bytes = 0) {
   if (m <= 0 || n <= 0) return;
   if (k <= 0 || k % G_BK != 0 || lda % 8 != 0 || ldb % 16 != 0 || blocksize < 64 || blocksize % 32 != 0 ||
       ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) {
     set_error(1, "gemm_4bit: requires k % 64 == 0, lda % 8 == 0, ldb % 16 == 0, 16-B aligned A/B, blocksize >= 64");
     return;
   }
-  // m = out features (weight rows), n = tokens.  Large problems: 256x256 tiles; small: 128x128.
+  // m = out features (weight rows), n = tokens.  Large problems: 256x256 tiles (split-K when the
+  // tile grid is too small and a workspace is given); small: 128x128.
   const long long tiles256 = (long long)((m + 255) / 256) * ((n + 255) / 256);
   const bool pow2_bs = (blocksize & (blocksize - 1)) == 0;
+  int ks = splitk_factor(m, n, k);
+  if (ws == nullptr || ((uintptr_t)ws & 15) || (long long)ks * m * n * (long long)sizeof(float) > ws_bytes) ks = 1;
   const bool use256 = pow2_bs && (g_tile_override == 256 ||
-                                  (g_tile_override != 128 && m >= 256 && n >= 256 && tiles256 >= 128));
+                                  (g_tile_override != 128 && m >= 256 && n >= 256 && tiles256 * ks >= 128));
   if (use256) {
-    launch_gemm_4bit_256<T>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
+    launch_gemm_4bit_256<T>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, ws, ks);
   } else {
     const int tiles = ((m + G_BN - 1) / G_BN) * ((n + G_BM - 1) / G_BM);
     hipLaunchKernelGGL((k_gemm_4bit<T>), dim3(tiles), dim3(G_THREADS), 0, current_stream(), m, n, k, A, B, absmax,
@@ -217,6 +239,19 @@ void cgemm_4bit_inference_code_bf16(int m, int n, int k, bf16_t* A, unsigned cha
                                     bf16_t* out, int lda, int ldb, int ldc, int blocksize) {
   gemm_4bit<bf16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
 }
+// [additive] the same with a caller-owned fp32 workspace that enables split-K for small tile grids
+// (size it with cgemm_4bit_workspace_bytes; a smaller or NULL workspace just disables split-K).
+void cgemm_4bit_inference_code_ws_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax,
+                                       float* datatype, fp16_t* out, int lda, int ldb, int ldc, int blocksize,
+                                       float* workspace, long long workspace_bytes) {
+  gemm_4bit<fp16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, workspace, workspace_bytes);
+}
+void cgemm_4bit_inference_code_ws_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, float* absmax,
+                                       float* datatype, bf16_t* out, int lda, int ldb, int ldc, int blocksize,
+                                       float* workspace, long long workspace_bytes) {
+  gemm_4bit<bf16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, workspace, workspace_bytes);
+}
+long long cgemm_4bit_workspace_bytes(int m, int n, int k) { return gemm_4bit_workspace_bytes(m, n, k); }
 
 }  // extern "C"
 

@@ -60,16 +60,19 @@ template <typename T>
 __global__ void __launch_bounds__(Q_THREADS, 1)
 k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B,
                 const float* __restrict__ absmax, const float* __restrict__ datatype, T* __restrict__ out,
-                int lda, int ldb, int ldc, int blocksize) {
+                int lda, int ldb, int ldc, int blocksize, float* __restrict__ ws, int ksplit) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[Q_LDS];
   float2* lut = reinterpret_cast<float2*>(smem + Q_OFF_L);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);        // provably wave-uniform (SGPR math)
   if (tid < 256) lut[tid] = make_float2(datatype[tid >> 4], datatype[tid & 15]);
 
-  // ---- tile order: XCD-contiguous ids, grouped 4 token-tiles x all feature-tiles
+  // ---- tile order: XCD-contiguous ids, grouped 4 token-tiles x all feature-tiles; with split-K
+  // (ksplit > 1) the split is the outer index, so an XCD's workgroups share one K range
   const int tilesN = (N + Q_BN - 1) / Q_BN, tilesM = (M + Q_BM - 1) / Q_BM;
-  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  const int ntiles = tilesN * tilesM;
+  const int wg_all = xcd_remap(blockIdx.x, ntiles * ksplit);
+  const int split = wg_all / ntiles, wg = wg_all - split * ntiles;
   constexpr int GROUP = 4;
   const int group_span = GROUP * tilesN;
   const int first_m = (wg / group_span) * GROUP;
@@ -91,13 +94,17 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
   const int bs_shift = __builtin_ctz(blocksize);                    // blocksize: power of two >= 64
   const long long abase = 2LL * ldb * min(n0 + arow, N - 1);        // element index of (row, k = 0)
 
-  const int nk = K / Q_BK;
+  // this workgroup's k-tiles: [kb, kb + nk) of the K / 64 (the host keeps ksplit <= K / 64)
+  const int nk_all = K / Q_BK;
+  const int kb = (int)((long long)split * nk_all / ksplit);
+  const int nk = (int)((long long)(split + 1) * nk_all / ksplit) - kb;
   auto dma_w = [&](int kt, int buf) {                               // packed weights + absmax of k-tile kt
+    kt += kb;
     glds16(psrc + (long long)kt * (Q_BK / 2), smem + Q_OFF_P + buf * Q_PT + wave * 1024);
     glds4(absmax + ((abase + (long long)kt * Q_BK) >> bs_shift), smem + Q_OFF_A + buf * Q_AT + wave * 256);
   };
   auto dma_x_piece = [&](int kt, int buf, int i) {
-    glds16(xsrc[i] + (long long)kt * Q_BK, smem + Q_OFF_X + buf * Q_XT + (4 * wave + i) * 1024);
+    glds16(xsrc[i] + (long long)(kb + kt) * Q_BK, smem + Q_OFF_X + buf * Q_XT + (4 * wave + i) * 1024);
   };
 
   // ---- dequant role: this thread owns 16 packed bytes (32 k) of one W row; 8 consecutive lanes take
@@ -180,6 +187,22 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
     __syncthreads();
   }
 
+  if (ksplit > 1) {
+    // split-K: fp32 partial tile -> ws[split][M][N]; k_splitk_reduce sums the splits in order
+    float* wsp = ws + (long long)split * M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + 128 * wm + 32 * i + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+          const int col = n0 + 64 * wn + 32 * j + (lane & 31);
+          if (row < M && col < N) wsp[(long long)row * N + col] = acc[i][j][r];
+        }
+    return;
+  }
+
   // ---- epilogue: acc -> LDS (per-wave [128][64] T, 136-B rows) -> 16-B coalesced stores
   uint8_t* ep = smem + wave * (128 * Q_EPI_STRIDE);
 #pragma unroll
@@ -212,17 +235,49 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
   }
 }
 
+// out[r, c] = T(sum_s ws[s][r][c]) in split order (fp32), one RNE cast
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_splitk_reduce(const float* __restrict__ ws, int ksplit, int rows, int cols, T* __restrict__ out, int ldc) {
+  const long long mn = (long long)rows * cols;
+  const long long i4 = 4LL * (blockIdx.x * 256LL + threadIdx.x);
+  if (i4 >= mn) return;
+  if ((cols & 3) == 0) {
+    float4 s = *reinterpret_cast<const float4*>(ws + i4);
+    for (int k = 1; k < ksplit; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + k * mn + i4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const long long r = i4 / cols, c = i4 - r * cols;
+    T* dst = out + r * ldc + c;
+    dst[0] = Io<T>::from_f32(s.x); dst[1] = Io<T>::from_f32(s.y);
+    dst[2] = Io<T>::from_f32(s.z); dst[3] = Io<T>::from_f32(s.w);
+  } else {
+    for (long long i = i4; i < i4 + 4 && i < mn; ++i) {
+      float s = ws[i];
+      for (int k = 1; k < ksplit; ++k) s += ws[k * mn + i];
+      const long long r = i / cols, c = i - r * cols;
+      out[r * ldc + c] = Io<T>::from_f32(s);
+    }
+  }
+}
+
 template <typename T>
 void launch_gemm_4bit_256(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype,
-                          T* out, int lda, int ldb, int ldc, int blocksize) {
+                          T* out, int lda, int ldb, int ldc, int blocksize, float* ws, int ksplit) {
   const long long tiles = (long long)((m + Q_BN - 1) / Q_BN) * ((n + Q_BM - 1) / Q_BM);
-  hipLaunchKernelGGL((k_gemm_4bit_256<T>), dim3((unsigned)tiles), dim3(Q_THREADS), 0, current_stream(), m, n, k, A, B,
-                     absmax, datatype, out, lda, ldb, ldc, blocksize);
+  hipLaunchKernelGGL((k_gemm_4bit_256<T>), dim3((unsigned)(tiles * ksplit)), dim3(Q_THREADS), 0, current_stream(), m,
+                     n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, ws, ksplit);
+  if (ksplit > 1) {
+    const long long mn = (long long)m * n;
+    hipLaunchKernelGGL((k_splitk_reduce<T>), dim3((unsigned)((mn / 4 + 255) / 256 + 1)), dim3(256), 0,
+                       current_stream(), ws, ksplit, n, m, out, ldc);
+  }
 }
 
 template void launch_gemm_4bit_256<bf16_t>(int, int, int, const bf16_t*, const uint8_t*, const float*, const float*,
-                                           bf16_t*, int, int, int, int);
+                                           bf16_t*, int, int, int, int, float*, int);
 template void launch_gemm_4bit_256<fp16_t>(int, int, int, const fp16_t*, const uint8_t*, const float*, const float*,
-                                           fp16_t*, int, int, int, int);
+                                           fp16_t*, int, int, int, int, float*, int);
 
 }  // namespace bnb

@@ -76,8 +76,10 @@ __device__ __forceinline__ int xcd_remap(int wg, int nwg) {
 
 extern int g_tile_override;   // 0 = auto, 128 / 256 = force that tile kernel (tests / A-B benchmarks)
 
+// ws/ksplit: split-K over ksplit workgroups per tile with fp32 partials in ws[ksplit][n][m]
+// (ksplit == 1: ws unused, direct T output)
 template <typename T>
 void launch_gemm_4bit_256(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype,
-                          T* out, int lda, int ldb, int ldc, int blocksize);
+                          T* out, int lda, int ldb, int ldc, int blocksize, float* ws, int ksplit);
 
 }  // namespace bnb

@@ -524,6 +524,21 @@ def gemm_4bit_supported(A: Tensor, state: QuantState) -> bool:
             and A.shape[-1] == state.shape[1] and state.blocksize >= 64)
 
 
+_GEMM_WS: dict = {}
+
+
+def _gemm_workspace(device, nbytes: int) -> Optional[Tensor]:
+    """Grow-only fp32 split-K workspace per device for gemm_4bit (cgemm_4bit_workspace_bytes); kept
+    across calls so steady-state calls (and HIP-graph replays) allocate nothing."""
+    if nbytes <= 0:
+        return None
+    ws = _GEMM_WS.get(device)
+    if ws is None or ws.numel() * 4 < nbytes:
+        ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
+        _GEMM_WS[device] = ws
+    return ws
+
+
 def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = None,
               absmax: Optional[Tensor] = None) -> Tensor:
     """Fused 4-bit weight GEMM for any number of activation rows (the M>1 slot of
@@ -544,10 +559,12 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     Bc = B if B.is_contiguous() else B.contiguous()
     prev_device = pre_call(A.device)
     is_on_gpu([A2, Bc, absmax, out, state.code])
-    fn = lib.cgemm_4bit_inference_code_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_4bit_inference_code_fp16
+    ws_bytes = int(lib.cgemm_4bit_workspace_bytes(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K)))
+    ws = _gemm_workspace(A.device, ws_bytes)
+    fn = lib.cgemm_4bit_inference_code_ws_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_4bit_inference_code_ws_fp16
     fn(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K), get_ptr(A2), get_ptr(Bc), get_ptr(absmax),
        get_ptr(state.code), get_ptr(out), ct.c_int32(K), ct.c_int32((K + 1) // 2), ct.c_int32(N),
-       ct.c_int32(state.blocksize))
+       ct.c_int32(state.blocksize), get_ptr(ws), ct.c_longlong(ws_bytes))
     post_call(prev_device)
     return out.view(*A.shape[:-1], N)
 

@@ -93,6 +93,16 @@ void cgemm_4bit_inference_code_fp16(int m, int n, int k, bnb_fp16* A, unsigned c
                                     bnb_fp16* out, int lda, int ldb, int ldc, int blocksize);
 void cgemm_4bit_inference_code_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, float* absmax, float* datatype,
                                     bnb_bf16* out, int lda, int ldb, int ldc, int blocksize);
+/* [additive] the same with a caller-owned fp32 workspace that lets small tile grids (narrow column
+ * shards) run split-K on the 256x256 kernel; size it with cgemm_4bit_workspace_bytes (0 = split-K
+ * not used for this shape).  A NULL or smaller workspace falls back to the unsplit kernels. */
+void cgemm_4bit_inference_code_ws_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, float* absmax,
+                                       float* datatype, bnb_fp16* out, int lda, int ldb, int ldc, int blocksize,
+                                       float* workspace, long long workspace_bytes);
+void cgemm_4bit_inference_code_ws_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, float* absmax,
+                                       float* datatype, bnb_bf16* out, int lda, int ldb, int ldc, int blocksize,
+                                       float* workspace, long long workspace_bytes);
+long long cgemm_4bit_workspace_bytes(int m, int n, int k);
 /* [additive, testing] force the GEMM tile kernel: 0 = auto, 128 = 128x128, 256 = 256x256 */
 void cgemm_4bit_set_tile(int tile);
 

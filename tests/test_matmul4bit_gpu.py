@@ -175,6 +175,51 @@ def test_gemm_4bit_tile_kernels_agree_large(dev):
     assert (Y.float() - Y1.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Yref.abs().max().item()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mnk,ks", [((1024, 512, 4096), 8), ((300, 264, 1088), 2), ((256, 384, 1024), 2)])
+def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
+    """Split-K on the 256x256 kernel (small tile grids, e.g. narrow column shards): fp32 partials in a
+    caller workspace, summed in split order, one cast.  Same tolerance as the unsplit kernel."""
+    F = _F()
+    M, N, K = mnk
+    assert F.lib.cgemm_4bit_workspace_bytes(N, M, K) == ks * M * N * 4
+    torch.manual_seed(M + 7 * N)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
+    Y = F.gemm_4bit(X, q, st)
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), st.absmax.cpu().numpy(), N, K, 64,
+                                    st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
+    assert frac == 0.0, err
+    # without a workspace the dispatcher falls back to an unsplit kernel: same result up to fp32 order
+    out = torch.empty_like(Y)
+    fn = F.lib.cgemm_4bit_inference_code_bf16 if dtype == torch.bfloat16 else F.lib.cgemm_4bit_inference_code_fp16
+    fn(ct.c_int32(N), ct.c_int32(M), ct.c_int32(K), F.get_ptr(X), F.get_ptr(q), F.get_ptr(st.absmax),
+       F.get_ptr(st.code), F.get_ptr(out), ct.c_int32(K), ct.c_int32(K // 2), ct.c_int32(N), ct.c_int32(64))
+    torch.cuda.synchronize()
+    rms = Y.float().pow(2).mean().sqrt().item()
+    assert (Y.float() - out.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Y.float().abs().max().item()
+
+
+def test_gemm_4bit_split_k_metric_shard(dev):
+    """The 8-way column shard of the metric shape (M=4096, N/8=512, K=11008): split-K result vs the
+    dequantize_4bit + fp32 matmul reference path."""
+    F = _F()
+    M, N, K = 4096, 512, 11008
+    assert F.lib.cgemm_4bit_workspace_bytes(N, M, K) > 0
+    torch.manual_seed(5)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    Y = F.gemm_4bit(X, q, st)
+    Yref = X.float() @ F.dequantize_4bit(q, st).float().t()
+    rms = Yref.pow(2).mean().sqrt().item()
+    assert (Y.float() - Yref).abs().max().item() < 2e-2 * rms + 2e-2 * Yref.abs().max().item()
+    assert (Y.float() - Yref).abs().mean().item() < 0.115
+
+
 def test_gemm_4bit_legacy_abi_nf4_fp16(dev):
     """cgemm_4bit_inference (ref ABI slot, fp16, NF4 hard-coded)."""
     F = _F()
