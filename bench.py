@@ -32,6 +32,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import python_src_quants.functional as F  # noqa: E402
+from python_src_quants.parallel import sharded_forward_overlapped  # noqa: E402
 
 M, N, K = 4096, 4096, 11008
 BS = 64
@@ -184,11 +185,14 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
             "dequant_cpu_gbs": n_el * 9 / t_deq / 1e9}
 
 
-def gemm_kernel_name(m, n):
-    """Which tile kernel gemm_4bit dispatches to (gemm4bit.hip: 256x256 when both sides >= 256 and the
-    256-tile grid still has >= 128 workgroups)."""
+def gemm_kernel_name(m, n, k=K):
+    """Which tile kernel gemm_4bit dispatches to for m tokens x n features (gemm4bit.hip: 256x256 when both
+    sides >= 256 and the grid, with split-K when the caller gives a workspace, has >= 128 workgroups)."""
+    ks = max(1, F.lib.cgemm_4bit_workspace_bytes(ct.c_int32(n), ct.c_int32(m), ct.c_int32(k)) // (4 * m * n))
     tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
-    return "k_gemm_4bit_256<bf16>" if (m >= 256 and n >= 256 and tiles256 >= 128) else "k_gemm_4bit<bf16>"
+    if m >= 256 and n >= 256 and tiles256 * ks >= 128:
+        return "k_gemm_4bit_256<bf16>" + (f" split-K x{ks} + k_splitk_reduce" if ks > 1 else "")
+    return "k_gemm_4bit<bf16>"
 
 
 def load_pmc_traffic():
@@ -210,6 +214,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip int8/decode/config-1/cpu legs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
+    ap.add_argument("--chunks", type=int, default=2,
+                    help="N>1: token-row chunks whose all-gathers overlap the next chunk's GEMM")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -230,27 +236,40 @@ def main():
     q, st = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True)
     del W
     Y = torch.empty(M, shard, device=dev, dtype=torch.bfloat16)
-    gathered = torch.empty(world * M, shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
+    chunks = args.chunks if (world > 1 and args.chunks >= 1 and M % args.chunks == 0) else 1
+    Mc = M // chunks
+    gathered = torch.empty(chunks, world, Mc, shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
     kev = []
 
     def step(record=False):
         absmax = F._absmax_fp32(st)                 # nested stats -> fp32 absmax (2 small launches)
-        if record:
-            s, e = _events()
-            s.record()
-        F.gemm_4bit(X, q, st, out=Y, absmax=absmax)
-        if record:
-            e.record()
-            kev.append((s, e))
+        ev = []
+
+        def mm(xc, yc):
+            if record:
+                s, e = _events()
+                s.record()
+            r = F.gemm_4bit(xc, q, st, out=yc, absmax=absmax)
+            if record:
+                e.record()
+                ev.append((s, e))
+            return r
         if world > 1:
-            dist.all_gather_into_tensor(gathered, Y)
+            # chunk c's RCCL all-gather (own stream) overlaps chunk c+1's GEMM; all waited at the end
+            sharded_forward_overlapped(X, mm, world, None, chunks, out=gathered, y=Y)
+        else:
+            mm(X, Y)
+        if record:
+            kev.append(ev)
 
     # clock ramp: MI355X takes ~0.1-0.3 s of sustained MFMA load to reach its steady clock; run the
     # step untimed for --prewarm-ms before the W counted warmup steps (the timed region is unchanged)
     # (GEMM only: a time-based loop must not contain a collective, ranks could disagree on its count)
     t_end = time.perf_counter() + args.prewarm_ms / 1e3
     while time.perf_counter() < t_end:
-        F.gemm_4bit(X, q, st, out=Y, absmax=F._absmax_fp32(st))
+        am = F._absmax_fp32(st)
+        for c in range(chunks):
+            F.gemm_4bit(X[c * Mc:(c + 1) * Mc], q, st, out=Y[c * Mc:(c + 1) * Mc], absmax=am)
         torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
@@ -273,8 +292,9 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     total_flops = 2.0 * M * N * K
     value = total_flops / (elapsed / args.steps) / 1e12
-    kern_s = sum(s.elapsed_time(e) for s, e in kev) / len(kev) * 1e-3
-    shard_flops = 2.0 * M * shard * K
+    # mean GEMM launch (one per chunk; with split-K it includes the reduce)
+    kern_s = sum(sum(s.elapsed_time(e) for s, e in ev) for ev in kev) / sum(len(ev) for ev in kev) * 1e-3
+    shard_flops = 2.0 * Mc * shard * K
     achieved = shard_flops / kern_s / 1e12
 
     extras = {}
@@ -293,7 +313,7 @@ def main():
     if rank == 0:
         pmc = load_pmc_traffic()
         traffic = None
-        if pmc and pmc.get("kernel") == gemm_kernel_name(M, shard) and pmc.get("shape") == [M, shard, K]:
+        if pmc and pmc.get("kernel") == gemm_kernel_name(Mc, shard) and pmc.get("shape") == [Mc, shard, K]:
             traffic = pmc.get("hbm_bytes_per_launch")
         line = {
             "metric": "NF4 matmul TFLOPS + INT8 igemmlt TOPS @ 4096x4096x11008, 1/2/4/8 GPU",
@@ -311,10 +331,11 @@ def main():
             "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (fused dequant+MFMA) "
                                    "+ bf16 all-gather of output-column shards",
                        "M": M, "N": N, "K": K, "blocksize": BS, "quant_type": "nf4", "compress_statistics": True,
-                       "parallelism": f"column-shard x{world} + RCCL all_gather" if world > 1 else "single GPU"},
+                       "parallelism": (f"column-shard x{world} + RCCL all_gather, {chunks} token-row chunks "
+                                       "(chunk c's all-gather overlaps chunk c+1's GEMM)") if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                         "kernel": gemm_kernel_name(M, shard), "kernel_us": round(kern_s * 1e6, 2),
+                         "kernel": gemm_kernel_name(Mc, shard), "kernel_us": round(kern_s * 1e6, 2),
                          "flops_per_launch": shard_flops},
             "cpu_baseline": cpu,
         }

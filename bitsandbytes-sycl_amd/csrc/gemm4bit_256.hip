@@ -56,11 +56,12 @@ template <> __device__ __forceinline__ uint32_t cvt2<bf16_t>(float lo, float hi)
 }
 template <> __device__ __forceinline__ uint32_t cvt2<fp16_t>(float lo, float hi) { return Mfma<fp16_t>::pack2(lo, hi); }
 
-template <typename T>
+template <typename T, bool SPLIT>
 __global__ void __launch_bounds__(Q_THREADS, 1)
 k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B,
                 const float* __restrict__ absmax, const float* __restrict__ datatype, T* __restrict__ out,
-                int lda, int ldb, int ldc, int blocksize, float* __restrict__ ws, int ksplit) {
+                int lda, int ldb, int ldc, int blocksize, float* __restrict__ ws, int ksplit_arg) {
+  const int ksplit = SPLIT ? ksplit_arg : 1;    // the unsplit instance keeps the k-loop free of split terms
   __shared__ __attribute__((aligned(16))) uint8_t smem[Q_LDS];
   float2* lut = reinterpret_cast<float2*>(smem + Q_OFF_L);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -96,8 +97,8 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
 
   // this workgroup's k-tiles: [kb, kb + nk) of the K / 64 (the host keeps ksplit <= K / 64)
   const int nk_all = K / Q_BK;
-  const int kb = (int)((long long)split * nk_all / ksplit);
-  const int nk = (int)((long long)(split + 1) * nk_all / ksplit) - kb;
+  const int kb = SPLIT ? (int)((long long)split * nk_all / ksplit) : 0;
+  const int nk = SPLIT ? (int)((long long)(split + 1) * nk_all / ksplit) - kb : nk_all;
   auto dma_w = [&](int kt, int buf) {                               // packed weights + absmax of k-tile kt
     kt += kb;
     glds16(psrc + (long long)kt * (Q_BK / 2), smem + Q_OFF_P + buf * Q_PT + wave * 1024);
@@ -187,7 +188,7 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
     __syncthreads();
   }
 
-  if (ksplit > 1) {
+  if (SPLIT) {
     // split-K: fp32 partial tile -> ws[split][M][N]; k_splitk_reduce sums the splits in order
     float* wsp = ws + (long long)split * M * N;
 #pragma unroll
@@ -266,9 +267,12 @@ template <typename T>
 void launch_gemm_4bit_256(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype,
                           T* out, int lda, int ldb, int ldc, int blocksize, float* ws, int ksplit) {
   const long long tiles = (long long)((m + Q_BN - 1) / Q_BN) * ((n + Q_BM - 1) / Q_BM);
-  hipLaunchKernelGGL((k_gemm_4bit_256<T>), dim3((unsigned)(tiles * ksplit)), dim3(Q_THREADS), 0, current_stream(), m,
-                     n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, ws, ksplit);
-  if (ksplit > 1) {
+  if (ksplit <= 1) {
+    hipLaunchKernelGGL((k_gemm_4bit_256<T, false>), dim3((unsigned)tiles), dim3(Q_THREADS), 0, current_stream(), m, n,
+                       k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, ws, 1);
+  } else {
+    hipLaunchKernelGGL((k_gemm_4bit_256<T, true>), dim3((unsigned)(tiles * ksplit)), dim3(Q_THREADS), 0,
+                       current_stream(), m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, ws, ksplit);
     const long long mn = (long long)m * n;
     hipLaunchKernelGGL((k_splitk_reduce<T>), dim3((unsigned)((mn / 4 + 255) / 256 + 1)), dim3(256), 0,
                        current_stream(), ws, ksplit, n, m, out, ldc);

@@ -10,7 +10,7 @@ xGMI assembles [g, M, N/g] (bf16), viewed as [M, N] by `gathered_to_rows`.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Callable, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -52,6 +52,45 @@ def gather_columns(y_local: torch.Tensor, world: int, group=None, out: Optional[
     return out
 
 
+def _gather_async(out: torch.Tensor, y: torch.Tensor, group=None):
+    """Start the all-gather of y [Mc, n] into out [world, Mc, n]; returns the work handle."""
+    if dist.get_backend(group) == "gloo":
+        return dist.all_gather(list(out.unbind(0)), y, group=group, async_op=True)
+    return dist.all_gather_into_tensor(out, y, group=group, async_op=True)
+
+
+def sharded_forward_overlapped(x2: torch.Tensor, local_mm: Callable, world: int, group=None, chunks: int = 2,
+                               out: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Token-row-chunked sharded forward: the local GEMM of chunk c+1 runs while the all-gather of
+    chunk c is in flight (RCCL runs on its own stream; async_op handles order it after the GEMM that
+    produced the chunk and before the caller's next use).  local_mm(x_chunk, y_chunk_or_None) returns
+    this rank's [Mc, n] slice.  Returns [chunks, world, Mc, n] (chunk c = token rows c*Mc .. +Mc);
+    `chunked_to_rows` assembles [M, world*n].  chunks must divide M (else a single chunk is used)."""
+    M = x2.shape[0]
+    if chunks < 1 or M % chunks:
+        chunks = 1
+    Mc = M // chunks
+    works = []
+    for c in range(chunks):
+        rows = slice(c * Mc, (c + 1) * Mc)
+        yc = local_mm(x2[rows], None if y is None else y[rows])
+        if out is None:
+            out = torch.empty((chunks, world, Mc, yc.shape[1]), dtype=yc.dtype, device=yc.device)
+        if world == 1:
+            out[c, 0].copy_(yc)
+        else:
+            works.append(_gather_async(out[c], yc.contiguous(), group))
+    for w in works:
+        w.wait()
+    return out
+
+
+def chunked_to_rows(g: torch.Tensor) -> torch.Tensor:
+    """[chunks, world, Mc, n] -> [chunks*Mc, world*n] (a copy)."""
+    c, w, mc, n = g.shape
+    return g.permute(0, 2, 1, 3).reshape(c * mc, w * n)
+
+
 def gathered_to_rows(g: torch.Tensor) -> torch.Tensor:
     """[world, M, n] -> [M, world*n] (a copy; consumers that can index [world, M, n] should not call this)."""
     w, m, n = g.shape
@@ -79,6 +118,15 @@ class ColumnShardedLinear4bit(torch.nn.Module):
             return F.gemv_4bit(x2, self.qweight.t(), state=self.quant_state)
         return F.gemm_4bit(x2, self.qweight, self.quant_state)
 
-    def forward(self, x: torch.Tensor, assemble: bool = True) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, assemble: bool = True, chunks: int = 1) -> torch.Tensor:
+        """chunks > 1 overlaps the all-gather of each token-row chunk with the next chunk's GEMM
+        (result layout [chunks, world, M/chunks, n] when assemble=False)."""
+        if chunks > 1:
+            x2 = x.reshape(-1, self.in_features)
+
+            def mm(xc, yc):
+                return F.gemm_4bit(xc, self.qweight, self.quant_state, out=yc)
+            g = sharded_forward_overlapped(x2, mm, self.world, self.group, chunks)
+            return chunked_to_rows(g) if assemble else g
         g = gather_columns(self.forward_local(x), self.world, self.group)
         return gathered_to_rows(g) if assemble else g

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <type_traits>
 
 namespace bnb {
 hipStream_t current_stream() { return nullptr; }
@@ -45,14 +46,21 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(code, hc, 64, hipMemcpyHostToDevice));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  auto launch = [&](auto kern, uint16_t* Y) {
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
+  };
+  // the library kernel takes (ws, ksplit) as well
+  auto launch256 = [&](uint16_t* Y) {
+    hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t, false>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am,
+                       code, (bf16_t*)Y, K, K / 2, N, BS, (float*)nullptr, 1);
+  };
   auto run = [&](const char* name, auto kern, uint16_t* Y) {
-    for (int i = 0; i < 3; ++i)
-      hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
+    auto go = [&]() { if constexpr (std::is_same_v<decltype(kern), int>) launch256(Y); else launch(kern, Y); };
+    for (int i = 0; i < 3; ++i) go();
     CK(hipDeviceSynchronize());
     const int R = 30;
     CK(hipEventRecord(e0));
-    for (int i = 0; i < R; ++i)
-      hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
+    for (int i = 0; i < R; ++i) go();
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / R;
@@ -60,10 +68,9 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   // warm the clocks
-  for (int i = 0; i < 200; ++i)
-    hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y0, K, K / 2, N, BS);
+  for (int i = 0; i < 200; ++i) launch256(Y0);
   CK(hipDeviceSynchronize());
-  run("256 (LDS dequant)", k_gemm_4bit_256<bf16_t>, Y0);
+  run("256 (LDS dequant)", 0, Y0);
   run("rd (reg dequant)", k_gemm_4bit_rd<bf16_t, 0>, Y1);
   {
     std::vector<uint16_t> a((size_t)M * N), b((size_t)M * N);
@@ -83,7 +90,7 @@ int main(int argc, char** argv) {
   run("rd interleave setprio", k_gemm_4bit_rd<bf16_t, 20>, Y1);
   run("rd no-dma no-dequant", k_gemm_4bit_rd<bf16_t, 3>, Y1);
   run("rd interleave no-dma no-deq", k_gemm_4bit_rd<bf16_t, 19>, Y1);
-  run("256 (LDS dequant)", k_gemm_4bit_256<bf16_t>, Y0);
+  run("256 (LDS dequant)", 0, Y0);
   run("rd (reg dequant)", k_gemm_4bit_rd<bf16_t, 0>, Y1);
   return 0;
 }
