@@ -214,6 +214,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip int8/decode/config-1/cpu legs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, the product path); gloo only to rehearse N>1 ranks on one GPU")
     ap.add_argument("--chunks", type=int, default=2,
                     help="N>1: token-row chunks whose all-gathers overlap the next chunk's GEMM")
     args = ap.parse_args()
@@ -221,10 +223,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     assert N % world == 0
     shard = N // world
 
