@@ -4,6 +4,7 @@
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -I bitsandbytes-sycl_amd/csrc tools/gemm_lab2.hip
 #include "gemm4bit_256.hip"
 #include "gemm4bit_rd_lab.hip"
+#include "gemm4bit_w4_lab.hip"
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -54,8 +55,15 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t, false>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am,
                        code, (bf16_t*)Y, K, K / 2, N, BS, (float*)nullptr, 1);
   };
-  auto run = [&](const char* name, auto kern, uint16_t* Y) {
-    auto go = [&]() { if constexpr (std::is_same_v<decltype(kern), int>) launch256(Y); else launch(kern, Y); };
+  auto launchw4 = [&](auto kern, uint16_t* Y) {
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y, K, K / 2, N, BS);
+  };
+  auto run = [&](const char* name, auto kern, uint16_t* Y, bool w4 = false) {
+    auto go = [&]() {
+      if constexpr (std::is_same_v<decltype(kern), int>) launch256(Y);
+      else if (w4) launchw4(kern, Y);
+      else launch(kern, Y);
+    };
     for (int i = 0; i < 3; ++i) go();
     CK(hipDeviceSynchronize());
     const int R = 30;
@@ -70,9 +78,7 @@ int main(int argc, char** argv) {
   // warm the clocks
   for (int i = 0; i < 200; ++i) launch256(Y0);
   CK(hipDeviceSynchronize());
-  run("256 (LDS dequant)", 0, Y0);
-  run("rd (reg dequant)", k_gemm_4bit_rd<bf16_t, 0>, Y1);
-  {
+  auto agree = [&]() {
     std::vector<uint16_t> a((size_t)M * N), b((size_t)M * N);
     CK(hipMemcpy(a.data(), Y0, a.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(b.data(), Y1, b.size() * 2, hipMemcpyDeviceToHost));
@@ -85,12 +91,17 @@ int main(int argc, char** argv) {
       if (!(d <= 0.02 * fabs(x) + 0.05)) ++nbad;
     }
     printf("agreement: max|d| %.4g  max|ref| %.4g  mean|d| %.4g  bad %zu / %zu\n", maxd, maxa, sumd / a.size(), nbad, a.size());
-  }
-  run("rd interleave", k_gemm_4bit_rd<bf16_t, 16>, Y0);
-  run("rd interleave setprio", k_gemm_4bit_rd<bf16_t, 20>, Y1);
-  run("rd no-dma no-dequant", k_gemm_4bit_rd<bf16_t, 3>, Y1);
-  run("rd interleave no-dma no-deq", k_gemm_4bit_rd<bf16_t, 19>, Y1);
+  };
   run("256 (LDS dequant)", 0, Y0);
+  run("w4 (1 wave/SIMD)", k_gemm_4bit_w4<bf16_t, 0>, Y1, true);
+  agree();
+  run("w4 setprio", k_gemm_4bit_w4<bf16_t, 4>, Y1, true);
+  agree();
+  run("w4 no-dma", k_gemm_4bit_w4<bf16_t, 1>, Y1, true);
+  run("w4 no-dequant", k_gemm_4bit_w4<bf16_t, 2>, Y1, true);
+  run("w4 no-dma no-deq", k_gemm_4bit_w4<bf16_t, 3>, Y1, true);
+  run("256 (LDS dequant)", 0, Y0);
+  run("w4 (1 wave/SIMD)", k_gemm_4bit_w4<bf16_t, 0>, Y1, true);
   run("rd (reg dequant)", k_gemm_4bit_rd<bf16_t, 0>, Y1);
   return 0;
 }

@@ -11,9 +11,11 @@ import python_src_quants.functional as F  # noqa: E402
 from python_src_quants.cextension import lib  # noqa: E402
 
 dev = torch.device("cuda", 0)
-M, K = 4096, 11008
-X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-for n in (4096, 2048, 1024, 512):
+K = 11008
+Xall = torch.randn(4096, K, device=dev, dtype=torch.bfloat16)
+for M, n in ((4096, 4096), (4096, 2048), (2048, 2048), (4096, 1024), (2048, 1024), (1024, 1024), (4096, 512),
+             (2048, 512), (1024, 512)):
+    X = Xall[:M]
     W = (torch.randn(n, K, device=dev) * 0.02).to(torch.bfloat16)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=False)
     Y = torch.empty(M, n, device=dev, dtype=torch.bfloat16)
@@ -30,5 +32,5 @@ for n in (4096, 2048, 1024, 512):
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / R * 1e3
-        print(f"N={n:5d} tile={tile:3d}  {us:8.1f} us  {2.0 * M * n * K / us / 1e6:7.1f} TFLOP/s", flush=True)
+        print(f"M={M:5d} N={n:5d} tile={tile:3d}  {us:8.1f} us  {2.0 * M * n * K / us / 1e6:7.1f} TFLOP/s", flush=True)
     lib.cgemm_4bit_set_tile(ct.c_int(0))
