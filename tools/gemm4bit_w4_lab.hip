@@ -1,7 +1,8 @@
 // DESIGN LAB (not built into the library): 256 x 256-tile fused 4-bit weight GEMM with ONE wave per
 // SIMD (4 waves x 512 VGPRs).  Round-1 result at 4096x4096x11008: 355-358 us vs 345-347 us for
 // csrc/gemm4bit_256.hip (profiles/lab/r01_nf4_gemm_designs_*.txt): 19 % more wave-cycles at a 16 %
-// higher clock.  Across the three designs MFMA-busy x clock stays ~1.0e9 MFMA-cycles/s per SIMD.  Wave w owns output columns n0 + 64w .. +63 for all 256 token rows:
+// higher clock.  Across the three designs MFMA-busy x clock stays ~1.0e9 MFMA-cycles/s per SIMD.
+// Wave w owns output columns n0 + 64w .. +63 for all 256 token rows:
 // 8 x 2 accumulators of v_mfma_f32_32x32x16 (256 VGPRs), so each A fragment read from LDS feeds two
 // MFMAs (half the LDS reads per MFMA of an 8-wave 256x256 tile) and the weights are dequantised in
 // the lane that feeds them to the MFMA (no LDS round trip of the dequantised tile).
