@@ -143,6 +143,36 @@ def bench_dequant_config1(dev, iters=30):
     return {"us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS, "bytes": nbytes}
 
 
+def bench_optimizer_8bit(dev, n=1 << 27, iters=10):
+    """Adam with 8-bit blockwise states (c<T>adam_8bit_blockwise_grad), HBM-bound.
+    Algorithmic bytes per element: g + p read, p write (sizeof T each), two state bytes read + written,
+    plus 2 x 4 B of absmax per 2048-element block read + written."""
+    res = {"n": n}
+    q1 = F.create_dynamic_map(signed=True).to(dev)
+    q2 = F.create_dynamic_map(signed=False).to(dev)
+    for dt, name in ((torch.float32, "fp32"), (torch.bfloat16, "bf16")):
+        g = torch.Generator(device=dev).manual_seed(9)
+        p = (torch.randn(n, device=dev, generator=g) * 0.1).to(dt)
+        grad = (torch.randn(n, device=dev, generator=g) * 0.01).to(dt)
+        s1 = torch.zeros(n, dtype=torch.uint8, device=dev)
+        s2 = torch.zeros(n, dtype=torch.uint8, device=dev)
+        blocks = (n + 2047) // 2048
+        a1 = torch.zeros(blocks, device=dev)
+        a2 = torch.zeros(blocks, device=dev)
+        step = [0]
+
+        def call():
+            step[0] += 1
+            F.optimizer_update_8bit_blockwise("adam", grad, p, s1, s2, 0.9, 0.999, 1e-8, step[0], 1e-3, q1, q2, a1, a2)
+        t = _time_loop(call, iters)
+        esz = p.element_size()
+        nbytes = n * (3 * esz + 4) + blocks * 16
+        res[name] = {"us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS,
+                     "bytes": nbytes}
+        del p, grad, s1, s2
+    return res
+
+
 def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
     """Reference CPU path as ported (oracle/cpu_ops_port.cpp, the restated cpu_ops.cpp dequantize_cpu,
     single-threaded as written) + torch CPU F.linear (the CPU path has no GEMM), on a
@@ -308,6 +338,7 @@ def main():
         extras["int8_igemmlt_config3"] = bench_int8(dev, 4096, 4096, 4096)
         extras["decode_gemv_config2"] = bench_decode_gemv(dev)
         extras["dequant_nf4_config1_gpu"] = bench_dequant_config1(dev)
+        extras["optimizer_adam8bit_blockwise"] = bench_optimizer_8bit(dev)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.no_extras:
         try:

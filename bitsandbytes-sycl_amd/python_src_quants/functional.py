@@ -846,3 +846,63 @@ def extract_outliers(A, SA, idx):
        ct.c_int32(shapeA[1]))
     post_call(prev_device)
     return out
+
+
+# ----------------------------------------------------------------------------- optimizers
+_OPT_NAMES = ("adam", "momentum", "rmsprop", "adagrad", "lion")
+# C-ABI names per optimizer and gradient dtype (fp32, fp16, bf16); the 32-bit names keep the
+# reference's mixed suffixes (ref:sycl/pythonInterface.cpp:230-241, python functional.py:29-56)
+_SUFFIX32 = {"adam": ("fp32", "fp16", "bf16"), "momentum": ("32", "16", "bf16"), "rmsprop": ("32", "16", "bf16"),
+             "adagrad": ("32", "16", "bf16"), "lion": ("fp32", "fp16", "bf16")}
+_DTYPE_INDEX = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+
+
+def _opt_fn(optimizer_name: str, g: Tensor, blockwise: bool):
+    name = "adam" if optimizer_name == "lamb" and not blockwise else optimizer_name
+    if name not in _OPT_NAMES or g.dtype not in _DTYPE_INDEX:
+        raise ValueError(f"Gradient+optimizer bit data type combination not supported: grad {g.dtype}, "
+                         f"optimizer {optimizer_name}")
+    i = _DTYPE_INDEX[g.dtype]
+    sym = (f"c{name}_8bit_blockwise_grad_{('fp32', 'fp16', 'bf16')[i]}" if blockwise
+           else f"c{name}32bit_grad_{_SUFFIX32[name][i]}")
+    return getattr(lib, sym)
+
+
+def optimizer_update_8bit_blockwise(optimizer_name: str, g: Tensor, p: Tensor, state1: Tensor,
+                                    state2: Optional[torch.Tensor], beta1: float, beta2: float, eps: float, step: int,
+                                    lr: float, qmap1: Tensor, qmap2: Optional[torch.Tensor], absmax1: Tensor,
+                                    absmax2: Optional[torch.Tensor], weight_decay: float = 0.0,
+                                    gnorm_scale: float = 1.0, skip_zeros=False) -> None:
+    """In-place optimizer step with 8-bit states quantised per 2048-element block with the dynamic
+    maps (ref:functional.py:1754-1814 -> c<name>_8bit_blockwise_grad_<T>)."""
+    if state1.dtype != torch.uint8:
+        raise ValueError(f"Gradient+optimizer bit data type combination not supported: grad {g.dtype}, "
+                         f"optimizer {state1.dtype}")
+    optim_func = _opt_fn(optimizer_name, g, True)
+    is_on_gpu([p, g, state1, state2, qmap1, qmap2, absmax1, absmax2])
+    prev_device = pre_call(g.device)
+    optim_func(get_ptr(p), get_ptr(g), get_ptr(state1), get_ptr(state2), ct.c_float(beta1), ct.c_float(beta2),
+               ct.c_float(eps), ct.c_int32(step), ct.c_float(lr), get_ptr(qmap1), get_ptr(qmap2), get_ptr(absmax1),
+               get_ptr(absmax2), ct.c_float(weight_decay), ct.c_float(gnorm_scale), ct.c_bool(skip_zeros),
+               ct.c_int32(g.numel()))
+    post_call(prev_device)
+
+
+def optimizer_update_32bit(optimizer_name: str, g: Tensor, p: Tensor, state1: Tensor, beta1: float, eps: float,
+                           step: int, lr: float, state2: Optional[torch.Tensor] = None, beta2: float = 0.0,
+                           weight_decay: float = 0.0, gnorm_scale: float = 1.0,
+                           unorm_vec: Optional[torch.Tensor] = None, max_unorm: float = 0.0,
+                           skip_zeros=False) -> None:
+    """In-place optimizer step with fp32 states (ref:functional.py:1526-1615 -> c<name>32bit_grad_<T>).
+    max_unorm > 0 (update-norm clipping, kPreconditionOptimizer32bit) is not supported here."""
+    if max_unorm > 0.0:
+        raise NotImplementedError("max_unorm > 0 is not supported by the MI355X backend")
+    optim_func = _opt_fn(optimizer_name, g, False)
+    param_norm = 0.0
+    is_on_gpu([g, p, state1, state2, unorm_vec])
+    prev_device = pre_call(g.device)
+    optim_func(get_ptr(g), get_ptr(p), get_ptr(state1), get_ptr(state2), get_ptr(unorm_vec), ct.c_float(max_unorm),
+               ct.c_float(param_norm), ct.c_float(beta1), ct.c_float(beta2), ct.c_float(eps),
+               ct.c_float(weight_decay), ct.c_int32(step), ct.c_float(lr), ct.c_float(gnorm_scale),
+               ct.c_bool(skip_zeros), ct.c_int32(g.numel()))
+    post_call(prev_device)

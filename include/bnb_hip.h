@@ -15,6 +15,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdbool.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -148,6 +149,102 @@ void cdequant_mm_int32_fp16(int* A, float* rowStats, float* colStats, bnb_fp16* 
 /* ---- outlier column gather: ref:sycl/pythonInterface.cpp:368-369 ---- */
 void cextractOutliers_turing(char* A, int* idx, char* out, int idx_size, int rows, int cols);   /* :368 */
 void cextractOutliers_ampere(char* A, int* idx, char* out, int idx_size, int rows, int cols);   /* :369 */
+
+/* ---- optimizers, SURVEY §8(f) row 4 (bnb_opt_T = float / bnb_fp16 / bnb_bf16 storage) ----
+ * 8-bit blockwise states, 2048-element blocks, dynamic maps: ref:sycl/pythonInterface.cpp:264-284
+ *   (kernels kernel_quant.cpp:2715-3208).  Adam uses state1+state2, the others state1 only.  */
+void cadam_8bit_blockwise_grad_fp32(float* p, float* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cadam_8bit_blockwise_grad_fp16(bnb_fp16* p, bnb_fp16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cadam_8bit_blockwise_grad_bf16(bnb_bf16* p, bnb_bf16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cmomentum_8bit_blockwise_grad_fp32(float* p, float* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cmomentum_8bit_blockwise_grad_fp16(bnb_fp16* p, bnb_fp16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cmomentum_8bit_blockwise_grad_bf16(bnb_bf16* p, bnb_bf16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void crmsprop_8bit_blockwise_grad_fp32(float* p, float* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void crmsprop_8bit_blockwise_grad_fp16(bnb_fp16* p, bnb_fp16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void crmsprop_8bit_blockwise_grad_bf16(bnb_bf16* p, bnb_bf16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cadagrad_8bit_blockwise_grad_fp32(float* p, float* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cadagrad_8bit_blockwise_grad_fp16(bnb_fp16* p, bnb_fp16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void cadagrad_8bit_blockwise_grad_bf16(bnb_bf16* p, bnb_bf16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void clion_8bit_blockwise_grad_fp32(float* p, float* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void clion_8bit_blockwise_grad_fp16(bnb_fp16* p, bnb_fp16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+void clion_8bit_blockwise_grad_bf16(bnb_bf16* p, bnb_bf16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
+        float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
+        float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+/* fp32 states: ref:sycl/pythonInterface.cpp:223-241 (reference suffixes; bf16 siblings additive).
+ * max_unorm > 0 is not supported (reported through cget_last_error). */
+void cadam32bit_grad_fp32(float* g, float* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cadam32bit_grad_fp16(bnb_fp16* g, bnb_fp16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cadam32bit_grad_bf16(bnb_bf16* g, bnb_bf16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cmomentum32bit_grad_32(float* g, float* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cmomentum32bit_grad_16(bnb_fp16* g, bnb_fp16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cmomentum32bit_grad_bf16(bnb_bf16* g, bnb_bf16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void crmsprop32bit_grad_32(float* g, float* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void crmsprop32bit_grad_16(bnb_fp16* g, bnb_fp16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void crmsprop32bit_grad_bf16(bnb_bf16* g, bnb_bf16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cadagrad32bit_grad_32(float* g, float* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cadagrad32bit_grad_16(bnb_fp16* g, bnb_fp16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void cadagrad32bit_grad_bf16(bnb_bf16* g, bnb_bf16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void clion32bit_grad_fp32(float* g, float* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void clion32bit_grad_fp16(bnb_fp16* g, bnb_fp16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
+void clion32bit_grad_bf16(bnb_bf16* g, bnb_bf16* p, float* state1, float* state2, float* unorm, float max_unorm,
+        float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
+        const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
 
 /* ---- [additive] runtime ---- */
 void cset_stream(void* stream);            /* hipStream_t used by every launch (NULL = null stream) */
