@@ -398,6 +398,36 @@ void dequantize_blockwise(const float* code, const uint8_t* A, const float* absm
   BNB_LAUNCH_CHECK("dequantize_blockwise");
 }
 
+// Nested statistics -> fp32 absmax in one pass: out[i] = code2[q[i]] * absmax2[i >> bs2_shift] + offset,
+// the fp32 product of dequantize_blockwise (kernel_quant.cpp:1430-1435) then the fp32 `absmax += offset`
+// of functional.py:1346-1350 (two roundings, as the two-step path).  16 codes per thread.
+__global__ void __launch_bounds__(256)
+k_dequantize_nested_absmax(const float* __restrict__ code2, const uint8_t* __restrict__ q, const float* __restrict__ absmax2,
+                           const float* __restrict__ offset, float* __restrict__ out, int bs2_shift, long long n) {
+  __shared__ float c2[256];
+  c2[threadIdx.x] = code2[threadIdx.x];
+  const float off = *offset;
+  __syncthreads();
+  const long long i0 = 16 * ((long long)blockIdx.x * 256 + threadIdx.x);
+  if (i0 >= n) return;
+  if (i0 + 16 <= n && (((uintptr_t)(q + i0)) & 15) == 0 && (((uintptr_t)(out + i0)) & 15) == 0) {
+    const uint4 v = *reinterpret_cast<const uint4*>(q + i0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float r[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const long long i = i0 + 4 * d + b;
+        r[b] = __fadd_rn(__fmul_rn(c2[(w[d] >> (8 * b)) & 0xFF], absmax2[i >> bs2_shift]), off);
+      }
+      reinterpret_cast<float4*>(out + i0)[d] = make_float4(r[0], r[1], r[2], r[3]);
+    }
+  } else {
+    for (long long i = i0; i < i0 + 16 && i < n; ++i) out[i] = __fadd_rn(__fmul_rn(c2[q[i]], absmax2[i >> bs2_shift]), off);
+  }
+}
+
 }  // namespace bnb
 
 using namespace bnb;
@@ -479,6 +509,21 @@ void cdequantize_blockwise_cpu_fp32(float* code, unsigned char* A, float* absmax
     hipStreamSynchronize(s);
   }
   hipFree(d_code); hipFree(d_A); hipFree(d_absmax); hipFree(d_out);
+}
+
+// [additive] nested statistics -> fp32 absmax in one launch (replaces dequantize_blockwise + the
+// offset add of functional.py:1346-1350); blocksize2 must be a power of two.
+void cdequantize_nested_absmax_fp32(float* code2, unsigned char* q, float* absmax2, float* offset, float* out,
+                                    int blocksize2, long long n) {
+  if (n <= 0) return;
+  if (blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1))) {
+    set_error(1, "dequantize_nested_absmax: blocksize2 must be a power of two");
+    return;
+  }
+  const unsigned grid = (unsigned)((n + 16 * 256 - 1) / (16 * 256));
+  hipLaunchKernelGGL(k_dequantize_nested_absmax, dim3(grid), dim3(256), 0, current_stream(), code2, q, absmax2, offset,
+                     out, __builtin_ctz(blocksize2), n);
+  BNB_LAUNCH_CHECK("dequantize_nested_absmax");
 }
 
 // Device-resident variant of the CPU-path dequantize (one byte per element, any blocksize);

@@ -428,6 +428,19 @@ def _absmax_fp32(state: QuantState) -> Tensor:
     """Per-block fp32 absmax, resolving nested statistics (ref:functional.py:1346-1350, 1982-1984)."""
     absmax = state.absmax
     if state.nested:
+        s2 = state.state2
+        bs2 = s2.blocksize
+        off = state.offset if isinstance(state.offset, torch.Tensor) else None
+        if (absmax.is_cuda and absmax.dtype == torch.uint8 and absmax.is_contiguous() and s2.absmax.dtype == torch.float32
+                and s2.code is not None and s2.code.is_cuda and off is not None and off.is_cuda
+                and off.dtype == torch.float32 and bs2 > 0 and (bs2 & (bs2 - 1)) == 0):
+            # one launch: code2[q] * absmax2 + offset (the two fp32 roundings of the two-step path)
+            out = torch.empty(absmax.numel(), dtype=torch.float32, device=absmax.device)
+            prev_device = pre_call(absmax.device)
+            lib.cdequantize_nested_absmax_fp32(get_ptr(s2.code), get_ptr(absmax), get_ptr(s2.absmax), get_ptr(off),
+                                               get_ptr(out), ct.c_int32(bs2), ct.c_longlong(absmax.numel()))
+            post_call(prev_device)
+            return out.view(absmax.shape)
         absmax = dequantize_blockwise(state.absmax, state.state2)
         absmax += state.offset
         if absmax.dtype != torch.float32:

@@ -246,6 +246,12 @@ void clion32bit_grad_bf16(bnb_bf16* g, bnb_bf16* p, float* state1, float* state2
         float param_norm, const float beta1, const float beta2, const float eps, const float weight_decay,
         const int step, const float lr, const float gnorm_scale, bool skip_zeros, const int n);
 
+/* ---- [additive] nested statistics -> fp32 absmax in one launch:
+ * out[i] = code2[q[i]] * absmax2[i / blocksize2] + *offset (fp32 product, then fp32 add), the result of
+ * dequantize_blockwise + `absmax += offset` (ref:python_src_quants/functional.py:1346-1350) ---- */
+void cdequantize_nested_absmax_fp32(float* code2, unsigned char* q, float* absmax2, float* offset, float* out,
+                                    int blocksize2, long long n);
+
 /* ---- [additive] runtime ---- */
 void cset_stream(void* stream);            /* hipStream_t used by every launch (NULL = null stream) */
 void* cget_stream(void);

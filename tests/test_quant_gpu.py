@@ -145,6 +145,25 @@ def test_functional_nested_matches_oracle(dev):
     full = F.dequantize_blockwise(st.absmax, st.state2) + st.offset
     exp = ref.nested_absmax(eq2, ea2, st.state2.code.cpu().numpy(), off)
     assert same_bits(full.cpu().numpy(), exp)
+    # the one-launch decode (cdequantize_nested_absmax_fp32) used by gemm_4bit gives the same bits
+    assert same_bits(F._absmax_fp32(st).cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("n", [1, 255, 4096 * 11008 // 64 + 3, 70001])
+def test_nested_absmax_one_launch_ragged(dev, n):
+    """cdequantize_nested_absmax_fp32 on ragged lengths and unaligned tails vs the oracle."""
+    F = _F()
+    rng = np.random.default_rng(n)
+    q = rng.integers(0, 256, n, dtype=np.uint8)
+    a2 = rng.uniform(0.01, 1.0, (n + 255) // 256).astype(np.float32)
+    code = F.create_dynamic_map(signed=True)
+    off = np.float32(0.0123)
+    out = torch.empty(n, device=dev)
+    tc, tq, ta2, toff = code.to(dev), torch.from_numpy(q).to(dev), torch.from_numpy(a2).to(dev), torch.tensor([off], device=dev)
+    F.lib.cdequantize_nested_absmax_fp32(F.get_ptr(tc), F.get_ptr(tq), F.get_ptr(ta2), F.get_ptr(toff), F.get_ptr(out),
+                                         ct.c_int32(256), ct.c_longlong(n))
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), ref.nested_absmax(q, a2, code.numpy(), off))
 
 
 def test_cpu_path_entry_points(golden, dev):

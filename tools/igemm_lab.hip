@@ -1,0 +1,191 @@
+// int8 GEMM design lab: the library's 256x256 kernel (csrc/igemm_256.hip: BK = 128, 2 LDS stages,
+// vmcnt(0) + __syncthreads per k-step) against a 3-stage variant (BK = 64 bytes, DMA two tiles ahead,
+// counted vmcnt, raw s_barrier) on the fused igemmlt + mm_dequant path, row-major A [M,K], B [N,K].
+// Outputs must be bit-identical (exact int32 + the same epilogue).  Usage: igemm_lab [M N K]
+#include "igemm_256.hip"
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace bnb {
+hipStream_t current_stream() { return nullptr; }
+void set_error(int, const char* what) { printf("error: %s\n", what); }
+
+constexpr int K3_BK = 64, K3_TILE = 256 * K3_BK, K3_STAGE = 2 * K3_TILE;   // 16 KiB per operand, 32 KiB per stage
+constexpr int K3_LDS = J_LDS_EPI > 3 * K3_STAGE ? J_LDS_EPI : 3 * K3_STAGE;
+
+// [rows][64 B] tile, 16-B slot s of row r at slot s ^ (((r >> 3) & 1) << 1): the ds_read_b128 lane
+// groups of a 16-row fragment read (rows l & 15, slot l >> 4) hit 16 distinct bank quads
+__device__ __forceinline__ int swz64(int r, int s) { return r * 64 + ((s ^ (((r >> 3) & 1) << 1)) << 4); }
+
+template <int FL>
+__global__ void __launch_bounds__(J_THREADS, 1)
+k_igemm_3s(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restrict__ B, fp16_t* __restrict__ out,
+           long long lda, long long ldb, long long ldc, const float* __restrict__ rowStats,
+           const float* __restrict__ colStats, const fp16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[K3_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (N + 255) / 256, tilesM = (M + 255) / 256;
+  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  constexpr int GROUP = 4;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  // DMA: piece p = 2*wave + i covers rows 16p .. 16p+15 (lane -> row 16p + (lane >> 2), LDS slot lane & 3)
+  const int8_t* asrc[2];
+  const int8_t* bsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (2 * wave + i) + (lane >> 2);
+    const int gslot = (lane & 3) ^ (((row >> 3) & 1) << 1);
+    asrc[i] = A + (long long)min(m0 + row, M - 1) * lda + 16 * gslot;
+    bsrc[i] = B + (long long)min(n0 + row, N - 1) * ldb + 16 * gslot;
+  }
+  const int nk = K / K3_BK;
+  auto dma = [&](int kt, int st) {
+    const long long k0 = (long long)min(kt, nk - 1) * K3_BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      glds16(asrc[i] + k0, smem + st * K3_STAGE + (2 * wave + i) * 1024);
+      glds16(bsrc[i] + k0, smem + st * K3_STAGE + K3_TILE + (2 * wave + i) * 1024);
+    }
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  i32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = i32x4_t{0, 0, 0, 0};
+
+  dma(0, 0);
+  dma(1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");     // tile 0 landed (tile 1 may be in flight)
+  __builtin_amdgcn_s_barrier();
+  int st = 0;
+  for (int t = 0; t < nk; ++t) {
+    int st2 = st + 2;
+    if (st2 >= 3) st2 -= 3;
+    dma(t + 2, st2);                                    // stage of tile t-1: every wave passed its reads
+    const uint8_t* as = smem + st * K3_STAGE;
+    const uint8_t* bs = as + K3_TILE;
+    const int slot = lane >> 4;
+    uint4 b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz64(64 * wn + 16 * j + (lane & 15), slot));
+    if (FL & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 a = *reinterpret_cast<const uint4*>(as + swz64(128 * wm + 16 * i + (lane & 15), slot));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a), __builtin_bit_cast(i32x4_t, b[j]),
+                                                          acc[i][j], 0, 0, 0);
+    }
+    if (FL & 1) __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // tile t+1 landed; tile t+2 stays in flight
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // this wave's LDS reads of tile t are done
+    __builtin_amdgcn_s_barrier();
+    st = st == 2 ? 0 : st + 1;
+  }
+  wait_vmcnt0();
+  __syncthreads();
+
+  // epilogue: fused mm_dequant (kernel_quant.cpp:3969 order), staged for 16-B stores
+  const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;
+  uint8_t* ep = smem + wave * (128 * J_EPI_STRIDE);
+  float cs[4], bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = min(gcol0 + 16 * j + (lane & 15), N - 1);
+    cs[j] = colStats[col];
+    bv[j] = bias ? (float)bias[col] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * i + 4 * (lane >> 4) + r;
+      const float rs = rowStats[min(grow0 + row, M - 1)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<fp16_t*>(ep + row * J_EPI_STRIDE + 2 * (16 * j + (lane & 15))) =
+            mm_dequant_value(acc[i][j][r], rs, cs[j], bv[j]);
+    }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = lane + 64 * it;
+    const int row = id >> 3, c8 = id & 7;
+    const int grow = grow0 + row, gcol = gcol0 + 8 * c8;
+    if (grow >= M || gcol + 8 > N) continue;
+    const uint2 lo = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8);
+    const uint2 hi = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8 + 8);
+    *reinterpret_cast<uint4*>(out + (long long)grow * ldc + gcol) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
+}  // namespace bnb
+using namespace bnb;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096, K = argc > 3 ? atoi(argv[3]) : 11008;
+  int8_t *A, *B;
+  fp16_t *C0, *C1;
+  float *rs, *cs;
+  CK(hipMalloc(&A, (size_t)M * K)); CK(hipMalloc(&B, (size_t)N * K));
+  CK(hipMalloc(&C0, (size_t)M * N * 2)); CK(hipMalloc(&C1, (size_t)M * N * 2));
+  CK(hipMalloc(&rs, M * 4)); CK(hipMalloc(&cs, N * 4));
+  {
+    std::vector<int8_t> h((size_t)std::max(M, N) * K);
+    srand(5);
+    for (auto& v : h) v = (int8_t)((rand() % 255) - 127);
+    CK(hipMemcpy(A, h.data(), (size_t)M * K, hipMemcpyHostToDevice));
+    for (auto& v : h) v = (int8_t)((rand() % 255) - 127);
+    CK(hipMemcpy(B, h.data(), (size_t)N * K, hipMemcpyHostToDevice));
+    std::vector<float> f(std::max(M, N));
+    for (auto& v : f) v = 0.5f + (rand() & 0xFFFF) / 65536.0f;
+    CK(hipMemcpy(rs, f.data(), M * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(cs, f.data(), N * 4, hipMemcpyHostToDevice));
+  }
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  auto lib = [&]() { launch_igemm_256<ROW, ROW, EPI_F16_ROW_DEQUANT>(M, N, K, A, B, C0, nullptr, K, K, N, rs, cs, nullptr); };
+  auto v3 = [&](auto kern) {
+    return [=]() { hipLaunchKernelGGL(kern, dim3(tiles), dim3(512), 0, 0, M, N, K, A, B, C1, (long long)K, (long long)K, (long long)N, rs, cs, (const fp16_t*)nullptr); };
+  };
+  auto time = [&](const char* name, auto fn) {
+    for (int i = 0; i < 3; ++i) fn();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 30; ++i) fn();
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / 30;
+    printf("%-22s %8.1f us  %7.1f TOPS\n", name, us, 2.0 * M * N * K / us / 1e6);
+    fflush(stdout);
+  };
+  for (int i = 0; i < 300; ++i) lib();
+  CK(hipDeviceSynchronize());
+  auto check = [&]() {
+    std::vector<uint16_t> a((size_t)M * N), b((size_t)M * N);
+    CK(hipMemcpy(a.data(), C0, a.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), C1, b.size() * 2, hipMemcpyDeviceToHost));
+    size_t diff = 0;
+    for (size_t i = 0; i < a.size(); ++i) diff += a[i] != b[i];
+    printf("  bit-identical: %s (%zu differ)\n", diff ? "NO" : "yes", diff);
+  };
+  for (int rep = 0; rep < 2; ++rep) {
+    time("lib 256 BK128 2-stage", lib);
+    time("3-stage BK64", v3(k_igemm_3s<0>));
+    check();
+    time("3-stage BK64 setprio", v3(k_igemm_3s<1>));
+    check();
+  }
+  return 0;
+}
