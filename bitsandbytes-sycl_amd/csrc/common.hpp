@@ -132,8 +132,10 @@ template <int DT> __device__ __forceinline__ uint32_t quant4(float x) {
   else return quantize_fp4(x);
 }
 
-// dQuantize<0>: binary search + midpoint rounding over a 256-entry code held in LDS
-__device__ __forceinline__ uint32_t quantize_dynamic8(const float* __restrict__ code, float x) {
+// dQuantize<0>: binary search + midpoint rounding over a 256-entry code held in LDS.  Code is a
+// plain pointer or a view with operator[] (e.g. DynMapView below).
+template <class Code>
+__device__ __forceinline__ uint32_t quantize_dynamic8(Code code, float x) {
   int pivot = 127, upper_pivot = 255, lower_pivot = 0;
   float lower = -1.0f, upper = 1.0f;
   float val = code[pivot];
@@ -158,6 +160,121 @@ __device__ __forceinline__ uint32_t quantize_dynamic8(const float* __restrict__ 
   } else {
     const float mid = __fmul_rn(__fadd_rn(lower, val), 0.5f);
     return x < mid ? lower_pivot : pivot;
+  }
+}
+
+// quantize_dynamic8 for N independent values, branch-free and level-synchronous: the N searches issue
+// their LDS reads of one level together (one lgkmcnt wait per level, not one per read; the scalar
+// form compiles to exec-masked branches with a full wait after every read).  Identical results: after
+// the last step (+-1) on the even pivot p the bracketing pivots are p + 1 and max(p - 1, 0), so the
+// midpoint pick reads code[p - 1], code[p], code[p + 1] once at the end and the search itself carries
+// only the pivot.  The first step's pivots (127, then 63 / 191) come from registers.
+// q[j] = code index; cq[j] = code[q[j]] (callers keep the sign of the value with it).
+template <int N, class Code>
+__device__ __forceinline__ void quantize_dynamic8_n(Code code, const float (&x)[N], uint32_t (&q)[N], float (&cq)[N]) {
+  const float c127 = code[127], c63 = code[63], c191 = code[191];
+  int pv[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const bool gt0 = x[j] > c127;
+    const bool gt1 = x[j] > (gt0 ? c191 : c63);
+    pv[j] = (gt0 ? 191 : 63) + (gt1 ? 32 : -32);
+  }
+#pragma unroll
+  for (int i = 16; i > 0; i >>= 1) {
+    float val[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) val[j] = code[pv[j]];
+#pragma unroll
+    for (int j = 0; j < N; ++j) pv[j] += x[j] > val[j] ? i : -i;
+  }
+  float lo[N], mid[N], hi[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) { lo[j] = code[max(pv[j] - 1, 0)]; mid[j] = code[pv[j]]; hi[j] = code[pv[j] + 1]; }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {                 // branch-free pick between p and its neighbour on x's side
+    const bool above = x[j] > mid[j];
+    const float nb = above ? hi[j] : lo[j];
+    const float m = __fmul_rn(__fadd_rn(nb, mid[j]), 0.5f);
+    const bool move = above ? (x[j] > m) : (x[j] < m);
+    q[j] = move ? (uint32_t)(above ? pv[j] + 1 : max(pv[j] - 1, 0)) : (uint32_t)pv[j];
+    cq[j] = move ? nb : mid[j];
+  }
+}
+
+// A 256-entry dynamic map laid out in LDS for the branch-free dQuantize<0> search (quantize_dynamic8
+// semantics for any sorted map: the same pivots and comparisons in the same order, stored differently).
+// 1024 floats (4 KiB), byte offsets:
+//      0  tree[i], i = 1..127: the search pivots in breadth-first (Eytzinger) order, tree[1] = code[127],
+//         children of node i at 2i and 2i + 1.  A level is a = 2a + (x > v ? 4 : 0) on the byte offset
+//         a = 4i (v_cmp, v_cndmask, v_lshl_or); one level's nodes are contiguous, so levels of <= 32
+//         nodes never bank-conflict.  After 7 levels a = 4 (128 + L) and the even pivot is p = 2L.
+//    512  code[2L]                             at byte a    (the final pick's records share the offset
+//   1024  code[max(2L - 1, 0)]                 at a + 512    a of the search: immediate ds_read
+//   1536  code[2L + 1]                         at a + 1024   offsets, no address arithmetic)
+//   2048  (code[max(2L-1,0)] + code[2L]) * 0.5 at a + 1536   the two midpoints of quantize_dynamic8,
+//   2560  (code[2L+1] + code[2L]) * 0.5        at a + 2048   rounded as it rounds them
+//   3072  code[c], c = 0..255                  (dequantisation)
+constexpr int DYNMAP_FLOATS = 1024;
+
+struct DynMapView {
+  const char* base;
+  __device__ __forceinline__ float at(int byte_off) const { return *reinterpret_cast<const float*>(base + byte_off); }
+  __device__ __forceinline__ float operator[](uint32_t c) const { return at(3072 + 4 * (int)c); }
+};
+
+// build the layout from a 256-entry global map (256 threads, 4 entries each; consecutive lanes write
+// consecutive dwords)
+__device__ __forceinline__ void dynmap_stage(float* table, const float* __restrict__ code) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int f = it * 256 + threadIdx.x, part = f >> 7, L = f & 127;
+    float v;
+    if (part == 0) {                             // tree node L (slot 0 unused)
+      const int i = max(L, 1), d = 31 - __builtin_clz(i);
+      v = code[((2 * (i - (1 << d)) + 1) << (7 - d)) - 1];
+    } else if (part == 1) {
+      v = code[2 * L];
+    } else if (part == 2) {
+      v = code[max(2 * L - 1, 0)];
+    } else if (part == 3) {
+      v = code[2 * L + 1];
+    } else if (part == 4) {
+      v = __fmul_rn(__fadd_rn(code[max(2 * L - 1, 0)], code[2 * L]), 0.5f);
+    } else if (part == 5) {
+      v = __fmul_rn(__fadd_rn(code[2 * L + 1], code[2 * L]), 0.5f);
+    } else {
+      v = code[f - 768];
+    }
+    table[f] = v;
+  }
+}
+
+// dQuantize<0> of N independent values, level-synchronous: q[j] = code index; with CQ, cq[j] = code[q[j]]
+template <int N, bool CQ>
+__device__ __forceinline__ void dynmap_quantize_n(DynMapView m, const float (&x)[N], uint32_t (&q)[N],
+                                                  float (&cq)[N]) {
+  const float root = m.at(4);
+  int a[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) a[j] = x[j] > root ? 12 : 8;
+#pragma unroll
+  for (int d = 1; d < 7; ++d) {
+    float v[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = m.at(a[j]);
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = 2 * a[j] + (x[j] > v[j] ? 4 : 0);
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float c = m.at(a[j]), mlo = m.at(a[j] + 1536), mhi = m.at(a[j] + 2048);
+    const bool up = x[j] > c;                    // quantize_dynamic8's tail, branch-free
+    const float th = up ? mhi : mlo;
+    const bool move = up ? (x[j] > th) : (x[j] < th);
+    const int p = (a[j] - 512) >> 1;
+    q[j] = (uint32_t)max(p + (move ? (up ? 1 : -1) : 0), 0);
+    if constexpr (CQ) cq[j] = move ? (up ? m.at(a[j] + 1024) : m.at(a[j] + 512)) : c;
   }
 }
 

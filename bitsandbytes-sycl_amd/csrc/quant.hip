@@ -98,8 +98,10 @@ k_quantize_blockwise(const float* __restrict__ code, const T* __restrict__ A, fl
     const float r = 1.0f / m;                        // IEEE reciprocal (kernel_quant.cpp:1304)
     if constexpr (DT == GENERAL8BIT) {
       uint32_t q[8];
+      float x[8], cq[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] = quantize_dynamic8(s_code, __fmul_rn(v[j], r));
+      for (int j = 0; j < 8; ++j) x[j] = __fmul_rn(v[j], r);
+      quantize_dynamic8_n<8>(s_code, x, q, cq);      // the 8 searches interleaved (common.hpp)
       if (VEC && e0 + 8 <= n) {
         uint2 w;
         w.x = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
