@@ -216,11 +216,15 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
 
 
 def gemm_kernel_name(m, n, k=K):
-    """Which tile kernel gemm_4bit dispatches to for m tokens x n features (gemm4bit.hip: 256x256 when both
-    sides >= 256 and the grid, with split-K when the caller gives a workspace, has >= 128 workgroups)."""
+    """Which kernel carries gemm_4bit's flops for m tokens x n features: from GEMM_4BIT_DEQUANT_MIN_ROWS
+    tokens the library GEMM after the dequantise kernel; below, gemm4bit.hip's 256x256 tile kernel when
+    the features are >= 256 and the grid (with split-K) has >= 128 workgroups, else the 128x128 one."""
+    if m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES:
+        return "hipBLASLt bf16 GEMM (Cijk_*, via torch.matmul) after k_dequantize_4bit_stream<bf16,NF4>"
     ks = max(1, F.lib.cgemm_4bit_workspace_bytes(ct.c_int32(n), ct.c_int32(m), ct.c_int32(k)) // (4 * m * n))
     tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
-    if m >= 256 and n >= 256 and tiles256 * ks >= 128:
+    tiles128 = ((m + 127) // 128) * ((n + 127) // 128)
+    if n >= 256 and 2 * tiles256 * ks >= tiles128:
         return "k_gemm_4bit_256<bf16>" + (f" split-K x{ks} + k_splitk_reduce" if ks > 1 else "")
     return "k_gemm_4bit<bf16>"
 
@@ -281,14 +285,7 @@ def main():
         ev = []
 
         def mm(xc, yc):
-            if record:
-                s, e = _events()
-                s.record()
-            r = F.gemm_4bit(xc, q, st, out=yc, absmax=absmax)
-            if record:
-                e.record()
-                ev.append((s, e))
-            return r
+            return F.gemm_4bit(xc, q, st, out=yc, absmax=absmax, events=ev if record else None)
         if world > 1:
             # chunk c's RCCL all-gather (own stream) overlaps chunk c+1's GEMM; all waited at the end
             sharded_forward_overlapped(X, mm, world, None, chunks, out=gathered, y=Y)
@@ -327,8 +324,13 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     total_flops = 2.0 * M * N * K
     value = total_flops / (elapsed / args.steps) / 1e12
-    # mean GEMM launch (one per chunk; with split-K it includes the reduce)
-    kern_s = sum(sum(s.elapsed_time(e) for s, e in ev) for ev in kev) / sum(len(ev) for ev in kev) * 1e-3
+    # mean duration per chunk of the stage that carries the flops (the fused kernel incl. any split-K
+    # reduce, or the library GEMM) and of the dequantise stage that precedes the library GEMM
+    def stage_mean(name):
+        d = [s.elapsed_time(e) for ev in kev for nm, s, e in ev if nm == name]
+        return sum(d) / len(d) * 1e-3 if d else None
+    kern_s = stage_mean("gemm")
+    deq_s = stage_mean("dequantize")
     shard_flops = 2.0 * Mc * shard * K
     achieved = shard_flops / kern_s / 1e12
 
@@ -364,15 +366,17 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (seeded randn; W ~ N(0,0.02) -> NF4 bs=64 nested stats; X ~ N(0,1) bf16)",
-            "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (fused dequant+MFMA) "
-                                   "+ bf16 all-gather of output-column shards",
+            "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (functional.gemm_4bit: HIP "
+                                   "dequantise + hipBLASLt bf16 GEMM at this M; fused dequant+MFMA kernel below "
+                                   f"{F.GEMM_4BIT_DEQUANT_MIN_ROWS} rows / {F.GEMM_4BIT_DEQUANT_MIN_FEATURES} features) + bf16 all-gather of output-column shards",
                        "M": M, "N": N, "K": K, "blocksize": BS, "quant_type": "nf4", "compress_statistics": True,
                        "parallelism": (f"column-shard x{world} + RCCL all_gather, {chunks} token-row chunks "
                                        "(chunk c's all-gather overlaps chunk c+1's GEMM)") if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                          "kernel": gemm_kernel_name(Mc, shard), "kernel_us": round(kern_s * 1e6, 2),
-                         "flops_per_launch": shard_flops},
+                         "flops_per_launch": shard_flops,
+                         "dequantize_us": round(deq_s * 1e6, 2) if deq_s else None},
             "cpu_baseline": cpu,
         }
         line.update(extras)

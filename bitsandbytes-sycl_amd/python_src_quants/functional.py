@@ -552,12 +552,36 @@ def _gemm_workspace(device, nbytes: int) -> Optional[Tensor]:
     return ws
 
 
+# From GEMM_4BIT_DEQUANT_MIN_ROWS activation rows and GEMM_4BIT_DEQUANT_MIN_FEATURES output features the
+# reference's own M > 1 algorithm -- dequantise the whole weight (our HIP kernel, HBM-bound) and run one
+# bf16/fp16 library GEMM (hipBLASLt) -- beats the fused kernel.  tools/gemm_baseline.py sweep, K = 11008
+# (fused vs dequantise + matmul, us): 4096 x 4096 331.7 vs 240.4; 2048 x 4096 189.2 vs 159.1;
+# 4096 x 1024 108.7 vs 95.0; 1024 x 4096 108.2 vs 106.2; 512 x 4096 67.6 vs 80.4; 4096 x 512 69.6 vs 70.8.
+GEMM_4BIT_DEQUANT_MIN_ROWS = 2048
+GEMM_4BIT_DEQUANT_MIN_FEATURES = 1024
+
+_DEQ_WS: dict = {}
+
+
+def _dequant_workspace(device, dtype, numel: int) -> Tensor:
+    """Grow-only weight buffer per (device, dtype) for the dequantise + library-GEMM path."""
+    key = (device, dtype)
+    ws = _DEQ_WS.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(numel, dtype=dtype, device=device)
+        _DEQ_WS[key] = ws
+    return ws[:numel]
+
+
 def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = None,
-              absmax: Optional[Tensor] = None) -> Tensor:
-    """Fused 4-bit weight GEMM for any number of activation rows (the M>1 slot of
-    cgemm_4bit_inference, ref:pythonInterface.cpp:377).  out[..., n] = A[..., :] @ W^T with W the
-    dequantised [N, K] weight; replaces dequantize_4bit + F.linear (autograd/_functions.py:507).
-    B is the packed uint8 weight (any view of the N*K/2 bytes)."""
+              absmax: Optional[Tensor] = None, events: Optional[list] = None) -> Tensor:
+    """4-bit weight GEMM for any number of activation rows (the M>1 slot of cgemm_4bit_inference,
+    ref:pythonInterface.cpp:377).  out[..., n] = A[..., :] @ W^T with W the dequantised [N, K] weight;
+    replaces dequantize_4bit + F.linear (autograd/_functions.py:507).  Large problems (see
+    GEMM_4BIT_DEQUANT_MIN_ROWS): the HIP dequantise kernel into a weight workspace + one hipBLASLt GEMM;
+    otherwise the fused kernel (dequantise in LDS + MFMA, split-K when the tile grid is small).
+    B is the packed uint8 weight (any view of the N*K/2 bytes).  events (bench instrumentation): a list
+    that receives (name, start, end) torch.cuda.Event pairs around the launched stages."""
     if not gemm_4bit_supported(A, state):
         raise ValueError("gemm_4bit: needs bf16/fp16 activations and in_features % 64 == 0")
     N, K = state.shape[0], state.shape[1]
@@ -572,6 +596,22 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     Bc = B if B.is_contiguous() else B.contiguous()
     prev_device = pre_call(A.device)
     is_on_gpu([A2, Bc, absmax, out, state.code])
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if events is not None else None
+    if ev:
+        ev[0].record()
+    if rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES:
+        W = _dequant_workspace(A.device, A.dtype, N * K).view(N, K)
+        qt = "fp4" if state.quant_type == "fp4" else "nf4"
+        getattr(lib, f"cdequantize_blockwise_{_QB[A.dtype]}_{qt}")(
+            get_ptr(None), get_ptr(Bc), get_ptr(absmax), get_ptr(W), ct.c_int(state.blocksize), ct.c_int(N * K))
+        post_call(prev_device)
+        if ev:
+            ev[1].record()
+        torch.matmul(A2, W.t(), out=out.view(rows, N))
+        if ev:
+            ev[2].record()
+            events += [("dequantize", ev[0], ev[1]), ("gemm", ev[1], ev[2])]
+        return out.view(*A.shape[:-1], N)
     ws_bytes = int(lib.cgemm_4bit_workspace_bytes(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K)))
     ws = _gemm_workspace(A.device, ws_bytes)
     fn = lib.cgemm_4bit_inference_code_ws_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_4bit_inference_code_ws_fp16
@@ -579,6 +619,9 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
        get_ptr(state.code), get_ptr(out), ct.c_int32(K), ct.c_int32((K + 1) // 2), ct.c_int32(N),
        ct.c_int32(state.blocksize), get_ptr(ws), ct.c_longlong(ws_bytes))
     post_call(prev_device)
+    if ev:
+        ev[2].record()
+        events.append(("gemm", ev[0], ev[2]))
     return out.view(*A.shape[:-1], N)
 
 

@@ -154,9 +154,11 @@ def test_gemm_4bit_each_tile_kernel(dev, tile, mnk):
     assert frac == 0.0, err
 
 
-def test_gemm_4bit_tile_kernels_agree_large(dev):
-    """Metric shape class: the 256x256 kernel (auto) equals the 128x128 kernel up to fp32 summation order."""
+def test_gemm_4bit_tile_kernels_agree_large(dev, monkeypatch):
+    """Metric shape class: the 256x256 kernel (auto) equals the 128x128 kernel up to fp32 summation order
+    (the fused kernel forced: at this size gemm_4bit would take the dequantise + library GEMM path)."""
     F = _F()
+    monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1 << 30)
     M, N, K = 2048, 2048, 11008
     torch.manual_seed(11)
     W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
@@ -176,7 +178,8 @@ def test_gemm_4bit_tile_kernels_agree_large(dev):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("mnk,ks", [((1024, 512, 4096), 8), ((300, 264, 1088), 2), ((256, 384, 1024), 2)])
+@pytest.mark.parametrize("mnk,ks", [((1024, 512, 4096), 8), ((300, 264, 1088), 2), ((256, 384, 1024), 2),
+                                    ((16, 1024, 2048), 4), ((3, 512, 1024), 2)])
 def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
     """Split-K on the 256x256 kernel (small tile grids, e.g. narrow column shards): fp32 partials in a
     caller workspace, summed in split order, one cast.  Same tolerance as the unsplit kernel."""
@@ -201,6 +204,36 @@ def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
     torch.cuda.synchronize()
     rms = Y.float().pow(2).mean().sqrt().item()
     assert (Y.float() - out.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Y.float().abs().max().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+def test_gemm_4bit_library_path(dev, dtype, qt):
+    """From GEMM_4BIT_DEQUANT_MIN_ROWS x GEMM_4BIT_DEQUANT_MIN_FEATURES gemm_4bit runs the reference's M > 1
+    algorithm on the GPU: the HIP dequantise kernel into a workspace, then one library GEMM.  Bit-equal to
+    dequantize_4bit + torch.matmul, within the GEMM tolerance of the oracle, and close to the fused kernel."""
+    F = _F()
+    M, N, K = 2048, 1024, 2048
+    assert M >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and N >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES
+    torch.manual_seed(17)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type=qt, compress_statistics=True)
+    Y = F.gemm_4bit(X, q, st)
+    assert torch.equal(Y, torch.matmul(X, F.dequantize_4bit(q, st).t()))
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64,
+                                    st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
+    assert frac == 0.0, err
+    F.GEMM_4BIT_DEQUANT_MIN_ROWS, saved = 1 << 30, F.GEMM_4BIT_DEQUANT_MIN_ROWS
+    try:
+        Yf = F.gemm_4bit(X, q, st)
+    finally:
+        F.GEMM_4BIT_DEQUANT_MIN_ROWS = saved
+    rms = Y.float().pow(2).mean().sqrt().item()
+    assert (Y.float() - Yf.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Y.float().abs().max().item()
 
 
 def test_gemm_4bit_split_k_metric_shard(dev):
