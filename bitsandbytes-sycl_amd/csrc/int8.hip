@@ -164,6 +164,97 @@ k_double_rowcol_quant(const fp16_t* __restrict__ A, const float* __restrict__ ro
   }
 }
 
+// ============================================================================ wide-tile stats + double quant
+// The threshold == 0 path (no outliers, no COO) on 16-B aligned rows with cols % 8 == 0: 32 x 512 tiles,
+// thread t owns 8 columns (t % 64) of the 8 rows (t / 64) + 4 i, so each thread keeps 8 x 16-B loads in
+// flight and each wave covers a whole 512-column row segment (row max by one wave reduction).  Column
+// atomics drop 2x (one per column per 32-row tile instead of per 16-row tile), row atomics 2x, and
+// workgroups carry 32 KiB instead of 8.  Same maxima / roundings as the 16 x 256 kernels above (the
+// max is order-free; the quantisation is the same expression per element).
+constexpr int W_ROWS = 32, W_COLS = 512;
+
+__global__ void __launch_bounds__(256)
+k_colrow_stats_wide(const fp16_t* __restrict__ A, float* __restrict__ rowStats, float* __restrict__ colStats,
+                    int rows, int cols, int col_tiles) {
+  __shared__ float s_col[4][W_COLS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row_tile = blockIdx.x / col_tiles, col_tile = blockIdx.x % col_tiles;
+  const int base_row = row_tile * W_ROWS, c0 = col_tile * W_COLS + 8 * lane;
+  const bool has_cols = c0 < cols;
+  uint4 raw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = base_row + wave + 4 * i;
+    raw[i] = (has_cols && row < rows) ? *reinterpret_cast<const uint4*>(A + (long long)row * cols + c0)
+                                      : make_uint4(0, 0, 0, 0);
+  }
+  float cmax[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cmax[j] = -3.402823466e+38f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+    const int row = base_row + wave + 4 * i;
+    const bool ok = has_cols && row < rows;
+    float rmax = -3.402823466e+38f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j >> 1] >> (16 * (j & 1))));
+      const float a = ok ? fabsf(v) : -3.402823466e+38f;
+      cmax[j] = fmaxf(cmax[j], a);
+      rmax = fmaxf(rmax, a);
+    }
+    rmax = wave_max_xor(rmax, 64);
+    if (lane == 0 && row < rows && rmax >= 0.0f) atomic_max_nonneg(&rowStats[row], rmax);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s_col[wave][8 * lane + j] = cmax[j];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int cl = tid + 256 * h;
+    const float m = fmaxf(fmaxf(s_col[0][cl], s_col[1][cl]), fmaxf(s_col[2][cl], s_col[3][cl]));
+    const int col = col_tile * W_COLS + cl;
+    if (col < cols && m >= 0.0f) atomic_max_nonneg(&colStats[col], m);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+k_double_rowcol_quant_wide(const fp16_t* __restrict__ A, const float* __restrict__ rowStats,
+                           const float* __restrict__ colStats, int8_t* __restrict__ out_col,
+                           int8_t* __restrict__ out_row, int rows, int cols, int col_tiles) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row_tile = blockIdx.x / col_tiles, col_tile = blockIdx.x % col_tiles;
+  const int base_row = row_tile * W_ROWS, c0 = col_tile * W_COLS + 8 * lane;
+  if (c0 >= cols) return;
+  uint4 raw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = base_row + wave + 4 * i;
+    if (row < rows) raw[i] = *reinterpret_cast<const uint4*>(A + (long long)row * cols + c0);
+  }
+  float cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = __fdiv_rn(127.0f, colStats[c0 + j]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = base_row + wave + 4 * i;
+    if (row >= rows) break;
+    const float rsc = __fdiv_rn(127.0f, rowStats[row]);
+    const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+    uint32_t qr[2] = {0, 0}, qc[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j >> 1] >> (16 * (j & 1))));
+      qr[j >> 2] |= (uint32_t)(uint8_t)rint_i8(__fmul_rn(v, rsc)) << (8 * (j & 3));
+      qc[j >> 2] |= (uint32_t)(uint8_t)rint_i8(__fmul_rn(v, cs[j])) << (8 * (j & 3));
+    }
+    const long long off = (long long)row * cols + c0;
+    *reinterpret_cast<uint2*>(out_row + off) = make_uint2(qr[0], qr[1]);
+    *reinterpret_cast<uint2*>(out_col + off) = make_uint2(qc[0], qc[1]);
+  }
+}
+
 // ============================================================================ layout transforms
 // One thread per element (row-major source index i).  These are load-time / small-tensor ops.
 
@@ -405,7 +496,11 @@ void cget_col_row_stats(fp16_t* A, float* rowStats, float* colStats, int* nnz_co
   if (rows <= 0 || cols <= 0) return;
   const int col_tiles = (cols + 255) / 256, row_tiles = (rows + 15) / 16;
   const bool vec = (((uintptr_t)A & 15) == 0) && (cols % 8 == 0);
-  if (nnz_threshold > 0.0f && nnz_count_row != nullptr)
+  if (vec && !(nnz_threshold > 0.0f && nnz_count_row != nullptr)) {
+    const int wct = (cols + W_COLS - 1) / W_COLS, wrt = (rows + W_ROWS - 1) / W_ROWS;
+    hipLaunchKernelGGL(k_colrow_stats_wide, dim3(wrt * wct), dim3(256), 0, current_stream(), A, rowStats, colStats,
+                       rows, cols, wct);
+  } else if (nnz_threshold > 0.0f && nnz_count_row != nullptr)
     hipLaunchKernelGGL(k_colrow_stats<true>, dim3(row_tiles * col_tiles), dim3(256), 0, current_stream(), A, rowStats,
                        colStats, nnz_count_row, nnz_threshold, rows, cols, col_tiles, vec);
   else
@@ -420,7 +515,11 @@ void cdouble_rowcol_quant(fp16_t* A, float* rowStats, float* colStats, char* out
   const int col_tiles = (cols + 255) / 256, row_tiles = (rows + 15) / 16;
   const bool vec = (((uintptr_t)A & 15) == 0) && (cols % 8 == 0) && (((uintptr_t)out_col_normed & 7) == 0) &&
                    (((uintptr_t)out_row_normed & 7) == 0);
-  if (threshold > 0.0f && rowidx && colidx && val && nnz_row_ptr)
+  if (vec && !(threshold > 0.0f && rowidx && colidx && val && nnz_row_ptr)) {
+    const int wct = (cols + W_COLS - 1) / W_COLS, wrt = (rows + W_ROWS - 1) / W_ROWS;
+    hipLaunchKernelGGL(k_double_rowcol_quant_wide, dim3(wrt * wct), dim3(256), 0, current_stream(), A, rowStats,
+                       colStats, (int8_t*)out_col_normed, (int8_t*)out_row_normed, rows, cols, wct);
+  } else if (threshold > 0.0f && rowidx && colidx && val && nnz_row_ptr)
     hipLaunchKernelGGL(k_double_rowcol_quant<true>, dim3(row_tiles * col_tiles), dim3(256), 0, current_stream(), A,
                        rowStats, colStats, (int8_t*)out_col_normed, (int8_t*)out_row_normed, rowidx, colidx, val,
                        nnz_row_ptr, threshold, rows, cols, col_tiles, vec);

@@ -864,10 +864,12 @@ def double_quant(A, col_stats=None, row_stats=None, out_col=None, out_row=None, 
     nnz_row_ptr = None
     if row_stats is None or col_stats is None:
         row_stats, col_stats, nnz_row_ptr = get_colrow_absmax(A, threshold=threshold)
+    # every element is written by the kernel (outliers as 0), so no zero-fill (the reference's torch.zeros
+    # costs two 1-byte-per-element fill passes: ~20 us at 4096 x 11008)
     if out_col is None:
-        out_col = torch.zeros(A.shape, device=device, dtype=torch.int8)
+        out_col = torch.empty(A.shape, device=device, dtype=torch.int8)
     if out_row is None:
-        out_row = torch.zeros(A.shape, device=device, dtype=torch.int8)
+        out_row = torch.empty(A.shape, device=device, dtype=torch.int8)
     coo_tensor = None
     prev_device = pre_call(A.device)
     is_on_gpu([A, col_stats, row_stats, out_col, out_row])

@@ -28,7 +28,8 @@ def test_double_quant_golden(golden, dev):
     assert same_bits(ocol.cpu().numpy(), golden["dq_col"])
 
 
-@pytest.mark.parametrize("shape", [(4096, 4096), (1, 7), (17, 300), (513, 1030), (2048, 11008)])
+@pytest.mark.parametrize("shape", [(4096, 4096), (1, 7), (17, 300), (513, 1030), (2048, 11008), (33, 520), (100, 1032),
+                                   (1, 8), (31, 4096)])
 def test_double_quant_random(dev, shape):
     F = _F()
     torch.manual_seed(shape[0])

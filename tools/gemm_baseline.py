@@ -67,6 +67,17 @@ def int8():
             print(f"{M}x{N}x{K} torch._int_mm (library) {t2:8.1f} us  {ops / t2 / 1e6:8.1f} TOPS", flush=True)
         except Exception as ex:  # noqa: BLE001
             print("torch._int_mm failed:", ex)
+        t_st = timeit(lambda: F.get_colrow_absmax(A))
+        rs_, cs_, _ = F.get_colrow_absmax(A)
+        t_dq = timeit(lambda: F.double_quant(A, col_stats=cs_, row_stats=rs_))
+        t_full = timeit(lambda: F.double_quant(A))
+
+        def fwd():
+            ca, _, sca, _, _ = F.double_quant(A)
+            F.igemmlt_dequant(ca, CB, sca, SCB, out=out)
+        t_fwd = timeit(fwd)
+        print(f"  colrow_stats {t_st:.1f} us, rowcol_quant {t_dq:.1f} us, double_quant {t_full:.1f} us, "
+              f"forward {t_fwd:.1f} us", flush=True)
         t3 = timeit(lambda: torch.matmul(A, Wt.t()))
         print(f"{M}x{N}x{K} fp16 matmul (library)   {t3:8.1f} us  {ops / t3 / 1e6:8.1f} TFLOP/s", flush=True)
 
