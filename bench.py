@@ -284,8 +284,13 @@ def main():
         absmax = F._absmax_fp32(st)                 # nested stats -> fp32 absmax (2 small launches)
         ev = []
 
-        def mm(xc, yc):
-            return F.gemm_4bit(xc, q, st, out=yc, absmax=absmax, events=ev if record else None)
+        first = [True]
+
+        def mm(xc, yc):   # chunks after the first reuse this step's dequantised shard (library path)
+            r = F.gemm_4bit(xc, q, st, out=yc, absmax=absmax, events=ev if record else None,
+                            reuse_weight=not first[0])
+            first[0] = False
+            return r
         if world > 1:
             # chunk c's RCCL all-gather (own stream) overlaps chunk c+1's GEMM; all waited at the end
             sharded_forward_overlapped(X, mm, world, None, chunks, out=gathered, y=Y)

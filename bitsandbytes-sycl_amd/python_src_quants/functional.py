@@ -561,6 +561,7 @@ GEMM_4BIT_DEQUANT_MIN_ROWS = 2048
 GEMM_4BIT_DEQUANT_MIN_FEATURES = 1024
 
 _DEQ_WS: dict = {}
+_DEQ_META: dict = {}
 
 
 def _dequant_workspace(device, dtype, numel: int) -> Tensor:
@@ -570,18 +571,22 @@ def _dequant_workspace(device, dtype, numel: int) -> Tensor:
     if ws is None or ws.numel() < numel:
         ws = torch.empty(numel, dtype=dtype, device=device)
         _DEQ_WS[key] = ws
+        _DEQ_META.pop(key, None)
     return ws[:numel]
 
 
 def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = None,
-              absmax: Optional[Tensor] = None, events: Optional[list] = None) -> Tensor:
+              absmax: Optional[Tensor] = None, events: Optional[list] = None, reuse_weight: bool = False) -> Tensor:
     """4-bit weight GEMM for any number of activation rows (the M>1 slot of cgemm_4bit_inference,
     ref:pythonInterface.cpp:377).  out[..., n] = A[..., :] @ W^T with W the dequantised [N, K] weight;
     replaces dequantize_4bit + F.linear (autograd/_functions.py:507).  Large problems (see
     GEMM_4BIT_DEQUANT_MIN_ROWS): the HIP dequantise kernel into a weight workspace + one hipBLASLt GEMM;
     otherwise the fused kernel (dequantise in LDS + MFMA, split-K when the tile grid is small).
     B is the packed uint8 weight (any view of the N*K/2 bytes).  events (bench instrumentation): a list
-    that receives (name, start, end) torch.cuda.Event pairs around the launched stages."""
+    that receives (name, start, end) torch.cuda.Event pairs around the launched stages.  reuse_weight:
+    the caller runs several row chunks of one product against the same, unmodified weight (the chunked
+    sharded forward); on the library path the workspace still holding this weight's dequantisation
+    from the previous call is used as is."""
     if not gemm_4bit_supported(A, state):
         raise ValueError("gemm_4bit: needs bf16/fp16 activations and in_features % 64 == 0")
     N, K = state.shape[0], state.shape[1]
@@ -601,16 +606,24 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         ev[0].record()
     if rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES:
         W = _dequant_workspace(A.device, A.dtype, N * K).view(N, K)
-        qt = "fp4" if state.quant_type == "fp4" else "nf4"
-        getattr(lib, f"cdequantize_blockwise_{_QB[A.dtype]}_{qt}")(
-            get_ptr(None), get_ptr(Bc), get_ptr(absmax), get_ptr(W), ct.c_int(state.blocksize), ct.c_int(N * K))
-        post_call(prev_device)
-        if ev:
+        key = (A.device, A.dtype)
+        meta = (Bc.data_ptr(), Bc._version, absmax.data_ptr(), absmax._version, N, K, state.blocksize,
+                state.quant_type)
+        if not (reuse_weight and _DEQ_META.get(key) == meta):
+            qt = "fp4" if state.quant_type == "fp4" else "nf4"
+            getattr(lib, f"cdequantize_blockwise_{_QB[A.dtype]}_{qt}")(
+                get_ptr(None), get_ptr(Bc), get_ptr(absmax), get_ptr(W), ct.c_int(state.blocksize), ct.c_int(N * K))
+            _DEQ_META[key] = meta
+            if ev:
+                ev[1].record()
+                events.append(("dequantize", ev[0], ev[1]))
+        elif ev:
             ev[1].record()
+        post_call(prev_device)
         torch.matmul(A2, W.t(), out=out.view(rows, N))
         if ev:
             ev[2].record()
-            events += [("dequantize", ev[0], ev[1]), ("gemm", ev[1], ev[2])]
+            events.append(("gemm", ev[1], ev[2]))
         return out.view(*A.shape[:-1], N)
     ws_bytes = int(lib.cgemm_4bit_workspace_bytes(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K)))
     ws = _gemm_workspace(A.device, ws_bytes)

@@ -124,8 +124,12 @@ class ColumnShardedLinear4bit(torch.nn.Module):
         if chunks > 1:
             x2 = x.reshape(-1, self.in_features)
 
-            def mm(xc, yc):
-                return F.gemm_4bit(xc, self.qweight, self.quant_state, out=yc)
+            first = [True]
+
+            def mm(xc, yc):   # one dequantisation of the shard per forward on the library path
+                r = F.gemm_4bit(xc, self.qweight, self.quant_state, out=yc, reuse_weight=not first[0])
+                first[0] = False
+                return r
             g = sharded_forward_overlapped(x2, mm, self.world, self.group, chunks)
             return chunked_to_rows(g) if assemble else g
         g = gather_columns(self.forward_local(x), self.world, self.group)

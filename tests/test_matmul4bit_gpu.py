@@ -282,3 +282,23 @@ def test_gemm_4bit_asymmetric_identity(dev):
     Y = F.gemm_4bit(X, q, st)
     Wd = F.dequantize_4bit(q, st)
     assert torch.equal(Y, Wd.t().contiguous())
+
+
+def test_gemm_4bit_reuse_weight_chunks(dev):
+    """Chunked forward on the library path: chunks after the first reuse the dequantised weight
+    (reuse_weight); the result equals the unchunked call, and a different weight is never reused."""
+    F = _F()
+    from python_src_quants.parallel import ColumnShardedLinear4bit
+    M, N, K = 4096, 1024, 2048
+    torch.manual_seed(23)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    lin = ColumnShardedLinear4bit(W, world=1, rank=0, device=dev)
+    full = F.gemm_4bit(X, lin.qweight, lin.quant_state)
+    chunked = lin.forward(X, chunks=2)
+    assert torch.equal(chunked, full)
+    # a second weight through the same workspace: reuse_weight must not hand back the first one
+    W2 = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    q2, st2 = F.quantize_4bit(W2, blocksize=64, quant_type="nf4", compress_statistics=True)
+    y2 = F.gemm_4bit(X[:2048], q2, st2, reuse_weight=True)
+    assert torch.equal(y2, torch.matmul(X[:2048], F.dequantize_4bit(q2, st2).t()))
