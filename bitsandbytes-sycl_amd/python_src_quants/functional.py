@@ -905,6 +905,61 @@ def double_quant(A, col_stats=None, row_stats=None, out_col=None, out_row=None, 
     return out_row, out_col, row_stats, col_stats, coo_tensor
 
 
+def spmm_coo(cooA: COOSparseTensor, B: Tensor, out: Optional[Tensor] = None) -> Tensor:
+    """out = A_coo @ B (fp16), ref:functional.py:2656-2701.  The reference routes this to a cuSPARSE
+    SpMM (cspmm_coo, left commented out in its C-ABI, Q18); here: the nonzeros are stably sorted by row,
+    row pointers built, and cspmm_coo_rows sums each row's products in fp32 in that order."""
+    if out is None:
+        out = torch.empty((cooA.rows, B.shape[1]), device=B.device, dtype=B.dtype)
+    nnz = cooA.nnz
+    assert cooA.rowidx.numel() == nnz and cooA.colidx.numel() == nnz and cooA.values.numel() == nnz
+    assert cooA.cols == B.shape[0]
+    assert B.dtype == torch.float16 and out.dtype == torch.float16
+    transposed_B = not B.is_contiguous()
+    ldb = B.stride()[1 if transposed_B else 0]
+    ldc = B.shape[1]
+    order = torch.sort(cooA.rowidx.long(), stable=True).indices
+    rows_sorted = cooA.rowidx[order]
+    colidx = cooA.colidx[order].contiguous()
+    values = cooA.values[order].contiguous()
+    row_ptr = torch.searchsorted(rows_sorted.long(), torch.arange(cooA.rows + 1, device=B.device)).int()
+    prev_device = pre_call(B.device)
+    is_on_gpu([row_ptr, colidx, values, B, out])
+    lib.cspmm_coo_rows(get_ptr(row_ptr), get_ptr(colidx), get_ptr(values), ct.c_int32(cooA.rows),
+                       ct.c_int32(B.shape[1]), ct.c_int32(ldb), get_ptr(B), ct.c_int32(ldc), get_ptr(out),
+                       ct.c_bool(transposed_B))
+    post_call(prev_device)
+    return out
+
+
+def spmm_coo_very_sparse(cooA: COOSparseTensor, B: Tensor, dequant_stats: Optional[Tensor] = None,
+                         out: Optional[Tensor] = None) -> Tensor:
+    """out += A_coo @ B for <= 32 nonzeros per row, ref:functional.py:2704-2782: one workgroup per nonzero
+    row (rows with most nonzeros first), fp16 accumulation; int8 B is dequantised by dequant_stats / 127."""
+    if out is None:
+        out = torch.zeros((cooA.rows, B.shape[1]), device=B.device, dtype=cooA.values.dtype)
+    nnz = cooA.nnz
+    prev_device = pre_call(B.device)
+    assert cooA.rowidx.numel() == nnz and cooA.colidx.numel() == nnz and cooA.values.numel() == nnz
+    assert cooA.cols == B.shape[0], f"{cooA.cols} vs {B.shape}"
+    if not B.is_contiguous():
+        raise ValueError("spmm_coo_very_sparse: B must be row-major contiguous (the kernel reads B rows)")
+    values, counts = torch.unique(cooA.rowidx, return_counts=True)
+    offset = counts.cumsum(0).int()
+    max_count, max_idx = torch.sort(counts, descending=True, stable=True)
+    max_idx = max_idx.int()
+    max_count = max_count.int()
+    assert max_count[0] <= 32, f"Current max count per row is 8 but found {max_count[0]}."
+    assert B.dtype in [torch.float16, torch.int8]
+    is_on_gpu([cooA.rowidx, cooA.colidx, cooA.values, B, out, dequant_stats])
+    fn = lib.cspmm_coo_very_sparse_naive_fp16 if B.dtype == torch.float16 else lib.cspmm_coo_very_sparse_naive_int8
+    fn(get_ptr(max_count), get_ptr(max_idx), get_ptr(offset), get_ptr(cooA.rowidx), get_ptr(cooA.colidx),
+       get_ptr(cooA.values), get_ptr(B), get_ptr(out), get_ptr(dequant_stats), ct.c_int32(counts.numel()),
+       ct.c_int32(nnz), ct.c_int32(cooA.rows), ct.c_int32(B.shape[1]), ct.c_int32(B.shape[1]))
+    post_call(prev_device)
+    return out
+
+
 def extract_outliers(A, SA, idx):
     """Gather int8 columns `idx` of a turing/ampere-tiled matrix (ref:functional.py:2914-2936)."""
     shapeA, formatA = SA[0], SA[1]

@@ -149,6 +149,20 @@ void cdequant_mm_int32_fp16(int* A, float* rowStats, float* colStats, bnb_fp16* 
 /* ---- outlier column gather: ref:sycl/pythonInterface.cpp:368-369 ---- */
 void cextractOutliers_turing(char* A, int* idx, char* out, int idx_size, int rows, int cols);   /* :368 */
 void cextractOutliers_ampere(char* A, int* idx, char* out, int idx_size, int rows, int cols);   /* :369 */
+/* COO sparse x dense: ref:sycl/pythonInterface.cpp:362-366 -> kspmm_coo_very_sparse_naive
+ * (kernel_gemm.cpp:1398-1545).  out (fp16 [rowsA, colsB]) += A_coo @ B, fp16 accumulation per nonzero;
+ * int8 B scaled by dequant_stats[col] / 127.  nnz, rowsA, rowsB kept for the reference's argument list. */
+void cspmm_coo_very_sparse_naive_fp16(int* max_count, int* max_idx, int* offset_rowidx, int* rowidx, int* colidx,
+        bnb_fp16* values, bnb_fp16* B, bnb_fp16* out, float* dequant_stats, int nnz_rows, int nnz, int rowsA,
+        int rowsB, int colsB);
+void cspmm_coo_very_sparse_naive_int8(int* max_count, int* max_idx, int* offset_rowidx, int* rowidx, int* colidx,
+        bnb_fp16* values, signed char* B, bnb_fp16* out, float* dequant_stats, int nnz_rows, int nnz, int rowsA,
+        int rowsB, int colsB);
+/* [additive] C = A_coo @ B over a row-sorted COO with row pointers (row_ptr[A_rows + 1]), fp32 accumulation;
+ * replaces cspmm_coo (pythonInterface.cpp:358-361, commented out in the reference, Q18), whose Python
+ * wrapper (functional.py:2656) targets a cuSPARSE SpMM. */
+void cspmm_coo_rows(int* row_ptr, int* A_colidx, bnb_fp16* A_vals, int A_rows, int B_cols, int ldb, bnb_fp16* B,
+        int ldc, bnb_fp16* C, bool transposed_B);
 
 /* ---- optimizers, SURVEY §8(f) row 4 (bnb_opt_T = float / bnb_fp16 / bnb_bf16 storage) ----
  * 8-bit blockwise states, 2048-element blocks, dynamic maps: ref:sycl/pythonInterface.cpp:264-284
