@@ -245,12 +245,29 @@ template <> struct Pack2<fp16_t> {
 // 256 contiguous bytes and every store instruction writes 1 KiB contiguous (8 outputs per lane).
 // All P loads (+ their absmax) are issued before any is consumed.  Values are fp32 code*absmax,
 // then one RNE cast -- identical to k_dequantize_blockwise.
-template <typename T, int DT, int P>
+// NESTED: the block statistics arrive compressed (compress_statistics=True) and are decoded in the
+// kernel, absmax = code2[q8[b]] * absmax2[b >> bs2_shift] + offset in fp32 (the dequantize_blockwise
+// product, then functional.py:1346-1350's `absmax += offset`), instead of a separate decode launch.
+struct NestedStats {
+  const uint8_t* q8;
+  const float* code2;
+  const float* absmax2;
+  const float* offset;
+  int bs2_shift;
+};
+
+template <typename T, int DT, int P, bool NESTED = false>
 __global__ void __launch_bounds__(256)
 k_dequantize_4bit_stream(const uint8_t* __restrict__ A, const float* __restrict__ absmax, T* __restrict__ out,
-                         int bs_shift, long long ndw) {
+                         int bs_shift, long long ndw, NestedStats ns = {}) {
   __shared__ float2 s_pair[256];
+  __shared__ float s_code2[NESTED ? 256 : 1];
   s_pair[threadIdx.x] = make_float2(code4_value<DT>(threadIdx.x >> 4), code4_value<DT>(threadIdx.x & 15));
+  float off = 0.0f;
+  if constexpr (NESTED) {
+    s_code2[threadIdx.x] = ns.code2[threadIdx.x];
+    off = *ns.offset;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t* Aw = reinterpret_cast<const uint32_t*>(A);
@@ -261,7 +278,12 @@ k_dequantize_4bit_stream(const uint8_t* __restrict__ A, const float* __restrict_
     for (int j = 0; j < P; ++j) {
       const long long d = min(base + 64LL * (P * wave + j) + lane, ndw - 1);
       w[j] = __builtin_nontemporal_load(Aw + d);
-      am[j] = absmax[(8 * d) >> bs_shift];
+      if constexpr (NESTED) {
+        const long long blk = (8 * d) >> bs_shift;
+        am[j] = __fadd_rn(__fmul_rn(s_code2[ns.q8[blk]], ns.absmax2[blk >> ns.bs2_shift]), off);
+      } else {
+        am[j] = absmax[(8 * d) >> bs_shift];
+      }
     }
 #pragma unroll
     for (int j = 0; j < P; ++j) {
@@ -400,6 +422,25 @@ void dequantize_blockwise(const float* code, const uint8_t* A, const float* absm
   BNB_LAUNCH_CHECK("dequantize_blockwise");
 }
 
+// 4-bit dequantise with compressed statistics in one launch; false when the shape needs the two-step path
+template <typename T, int DT>
+bool dequantize_4bit_nested(const uint8_t* A, const uint8_t* q8, const float* code2, const float* absmax2,
+                            const float* offset, T* out, int blocksize, int blocksize2, long long n) {
+  if (n <= 0) return true;
+  if (blocksize < 64 || (blocksize & (blocksize - 1)) || blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1)) ||
+      n % 8 != 0 || ((uintptr_t)A & 3) != 0 || !aligned16(out))
+    return false;
+  constexpr int P = BNB_DQ_P;
+  const long long ndw = n / 8;
+  const long long wgs = (ndw + 256 * P - 1) / (256 * P);
+  const int grid = (int)(wgs < 65536 ? wgs : 65536);
+  const NestedStats ns{q8, code2, absmax2, offset, __builtin_ctz(blocksize2)};
+  hipLaunchKernelGGL((k_dequantize_4bit_stream<T, DT, P, true>), dim3(grid), dim3(256), 0, current_stream(), A,
+                     nullptr, out, __builtin_ctz(blocksize), ndw, ns);
+  BNB_LAUNCH_CHECK("dequantize_4bit_nested");
+  return true;
+}
+
 // Nested statistics -> fp32 absmax in one pass: out[i] = code2[q[i]] * absmax2[i >> bs2_shift] + offset,
 // the fp32 product of dequantize_blockwise (kernel_quant.cpp:1430-1435) then the fp32 `absmax += offset`
 // of functional.py:1346-1350 (two roundings, as the two-step path).  16 codes per thread.
@@ -465,6 +506,20 @@ BNB_DEQUANT_ABI(cdequantize_blockwise_bf16_nf4, bf16_t, NF4)
 BNB_DEQUANT_ABI(cdequantize_blockwise_fp32, float, GENERAL8BIT)
 BNB_DEQUANT_ABI(cdequantize_blockwise_fp32_fp4, float, FP4)
 BNB_DEQUANT_ABI(cdequantize_blockwise_fp32_nf4, float, NF4)
+
+// [additive] 4-bit dequantise with compressed statistics decoded in the kernel (one launch instead of
+// the dequantize_blockwise of the absmax + the 4-bit dequantise, functional.py:1342-1350).  Returns 0 when
+// launched, 1 when the shape needs the two-step path.
+#define BNB_DEQUANT_NESTED_ABI(fname, T, DT)                                                                    \
+  int fname(unsigned char* A, unsigned char* absmax_q, float* code2, float* absmax2, float* offset, T* out,      \
+            int blocksize, int blocksize2, long long n) {                                                        \
+    return dequantize_4bit_nested<T, DT>(A, absmax_q, code2, absmax2, offset, out, blocksize, blocksize2, n) ? 0  \
+                                                                                                             : 1; \
+  }
+BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_fp16_fp4, fp16_t, FP4)
+BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_fp16_nf4, fp16_t, NF4)
+BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_bf16_fp4, bf16_t, FP4)
+BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_bf16_nf4, bf16_t, NF4)
 
 // Host-pointer entry points (ref:sycl/pythonInterface.cpp:419-420).  Executed on the current
 // GPU: stage -> kernel -> copy back (synchronous, like the reference CPU path).

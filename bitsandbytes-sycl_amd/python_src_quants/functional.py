@@ -448,6 +448,24 @@ def _absmax_fp32(state: QuantState) -> Tensor:
     return absmax
 
 
+def _dequant_4bit_nested(A: Tensor, state: QuantState, out: Tensor) -> bool:
+    """One launch: the 4-bit dequantise with the compressed statistics decoded in the kernel
+    (cdequantize_blockwise_nested_*).  False when the dtype/shape needs the two-step path."""
+    if out.dtype not in (torch.float16, torch.bfloat16) or state.absmax.dtype != torch.uint8:
+        return False
+    s2 = state.state2
+    offset = state.offset if torch.is_tensor(state.offset) else torch.tensor(float(state.offset))
+    offset = offset.to(device=A.device, dtype=torch.float32).reshape(1)
+    prev_device = pre_call(A.device)
+    is_on_gpu([A, state.absmax, s2.code, s2.absmax, offset, out])
+    qt = "fp4" if state.quant_type == "fp4" else "nf4"
+    fn = getattr(lib, f"cdequantize_blockwise_nested_{_QB[out.dtype]}_{qt}")
+    rc = fn(get_ptr(A), get_ptr(state.absmax), get_ptr(s2.code), get_ptr(s2.absmax), get_ptr(offset), get_ptr(out),
+            ct.c_int32(state.blocksize), ct.c_int32(s2.blocksize), ct.c_longlong(out.numel()))
+    post_call(prev_device)
+    return rc == 0
+
+
 def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, absmax: Optional[Tensor] = None,
                     out: Optional[Tensor] = None, blocksize: int = 64, quant_type="fp4") -> Tensor:
     """ref:functional.py:1291-1424"""
@@ -463,11 +481,15 @@ def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, absmax:
                                  quant_type=quant_type)
     else:
         absmax = quant_state.absmax
-    if quant_state.nested:
-        absmax = _absmax_fp32(quant_state)
     if out is None:
         out = torch.empty(quant_state.shape, dtype=quant_state.dtype, device=A.device)
     n = out.numel()
+    if quant_state.nested and _dequant_4bit_nested(A, quant_state, out):
+        if A.shape[0] == 1:   # is_transposed (ref:functional.py:1420-1424)
+            return out.t()
+        return out
+    if quant_state.nested:
+        absmax = _absmax_fp32(quant_state)
 
     prev_device = pre_call(A.device)
     is_on_gpu([A, absmax, out])
@@ -594,25 +616,31 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if not A2.is_contiguous() or A2.data_ptr() % 16:
         A2 = A2.contiguous()
     rows = A2.shape[0]
-    if absmax is None:
+    library = rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES
+    if absmax is None and not (library and state.nested):
         absmax = _absmax_fp32(state)
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
     prev_device = pre_call(A.device)
-    is_on_gpu([A2, Bc, absmax, out, state.code])
+    is_on_gpu([A2, Bc, out, state.code] + ([absmax] if absmax is not None else []))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if events is not None else None
     if ev:
         ev[0].record()
-    if rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES:
+    if library:
         W = _dequant_workspace(A.device, A.dtype, N * K).view(N, K)
         key = (A.device, A.dtype)
-        meta = (Bc.data_ptr(), Bc._version, absmax.data_ptr(), absmax._version, N, K, state.blocksize,
+        stats = absmax if absmax is not None else state.absmax
+        meta = (Bc.data_ptr(), Bc._version, stats.data_ptr(), stats._version, N, K, state.blocksize,
                 state.quant_type)
         if not (reuse_weight and _DEQ_META.get(key) == meta):
-            qt = "fp4" if state.quant_type == "fp4" else "nf4"
-            getattr(lib, f"cdequantize_blockwise_{_QB[A.dtype]}_{qt}")(
-                get_ptr(None), get_ptr(Bc), get_ptr(absmax), get_ptr(W), ct.c_int(state.blocksize), ct.c_int(N * K))
+            if absmax is None and not _dequant_4bit_nested(Bc, state, W):   # nested stats decoded in-kernel
+                absmax = _absmax_fp32(state)
+            if absmax is not None:
+                qt = "fp4" if state.quant_type == "fp4" else "nf4"
+                getattr(lib, f"cdequantize_blockwise_{_QB[A.dtype]}_{qt}")(
+                    get_ptr(None), get_ptr(Bc), get_ptr(absmax), get_ptr(W), ct.c_int(state.blocksize),
+                    ct.c_int(N * K))
             _DEQ_META[key] = meta
             if ev:
                 ev[1].record()

@@ -212,6 +212,17 @@ void clion_8bit_blockwise_grad_fp16(bnb_fp16* p, bnb_fp16* g, unsigned char* sta
 void clion_8bit_blockwise_grad_bf16(bnb_bf16* p, bnb_bf16* g, unsigned char* state1, unsigned char* state2, float beta1, float beta2,
         float eps, int step, float lr, float* quantiles1, float* quantiles2, float* absmax1, float* absmax2,
         float weight_decay, const float gnorm_scale, bool skip_zeros, int n);
+/* [additive] 4-bit dequantise with compressed statistics decoded in the kernel, absmax = code2[absmax_q[b]] *
+ * absmax2[b / blocksize2] + *offset (fp32): one launch instead of dequantize_blockwise(absmax) + the 4-bit
+ * dequantise (functional.py:1342-1350).  Returns 0 when launched, 1 when the shape needs the two-step path. */
+int cdequantize_blockwise_nested_fp16_fp4(unsigned char* A, unsigned char* absmax_q, float* code2, float* absmax2,
+        float* offset, bnb_fp16* out, int blocksize, int blocksize2, long long n);
+int cdequantize_blockwise_nested_fp16_nf4(unsigned char* A, unsigned char* absmax_q, float* code2, float* absmax2,
+        float* offset, bnb_fp16* out, int blocksize, int blocksize2, long long n);
+int cdequantize_blockwise_nested_bf16_fp4(unsigned char* A, unsigned char* absmax_q, float* code2, float* absmax2,
+        float* offset, bnb_bf16* out, int blocksize, int blocksize2, long long n);
+int cdequantize_blockwise_nested_bf16_nf4(unsigned char* A, unsigned char* absmax_q, float* code2, float* absmax2,
+        float* offset, bnb_bf16* out, int blocksize, int blocksize2, long long n);
 /* fp32 states: ref:sycl/pythonInterface.cpp:223-241 (reference suffixes; bf16 siblings additive).
  * max_unorm > 0 is not supported (reported through cget_last_error). */
 void cadam32bit_grad_fp32(float* g, float* p, float* state1, float* state2, float* unorm, float max_unorm,

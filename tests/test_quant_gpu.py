@@ -186,3 +186,22 @@ def test_cpu_path_entry_points(golden, dev):
     # the functional CPU route goes through the same entry points
     q2, st = F.quantize_blockwise(torch.from_numpy(golden["cpu_A"].copy()), blocksize=64)
     assert same_bits(q2.numpy(), golden["cpu_q"])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("shape,bs", [((1024, 4096), 64), ((300, 640), 128), ((7, 64 * 9), 64)])
+def test_dequantize_4bit_nested_one_launch(dev, dtype, qt, shape, bs):
+    """dequantize_4bit with compressed statistics runs one launch (cdequantize_blockwise_nested_*, absmax
+    decoded in the kernel) and gives the bits of the two-step path (fp32 absmax, then the 4-bit dequantise)."""
+    F = _F()
+    torch.manual_seed(shape[0] + bs)
+    w = torch.randn(*shape, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(w, blocksize=bs, quant_type=qt, compress_statistics=True)
+    one = F.dequantize_4bit(q, st)
+    am = F._absmax_fp32(st)
+    two = torch.empty_like(one)
+    getattr(F.lib, f"cdequantize_blockwise_{F._QB[dtype]}_{qt}")(F.get_ptr(None), F.get_ptr(q), F.get_ptr(am),
+                                                                  F.get_ptr(two), ct.c_int(bs), ct.c_int(two.numel()))
+    torch.cuda.synchronize()
+    assert torch.equal(one.view(torch.int16), two.view(torch.int16))
