@@ -1,224 +1,81 @@
-// Decode GEMV design lab: times kernel variants of the 4-bit M=1 product on synthetic data
-// (11008 x 4096 NF4 weight, bs 64, 14 rotating copies > MALL).  Not part of the library.
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -I../bitsandbytes-sycl_amd/csrc gemv_lab.hip -o gemv_lab
-#include <hip/hip_runtime.h>
-#include <cstdio>
+// Decode GEMV lab (11008 x 4096 NF4, bf16 activations, plain fp32 absmax): the library table/dot kernel
+// at several (R rows per wave, U chunk groups per lane) schedules, over 14 rotating weight copies (past
+// the 256 MB MALL).  Run under `rocprofv3 --kernel-trace --stats` for per-kernel durations; outputs are
+// checked against the library configuration (fp32 sums in a different order: tolerance, not bits).
+#include "gemv4bit.hip"
+#include <cmath>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
-#include "common.hpp"
-#include "gemm_common.hpp"
 
+namespace bnb {
+hipStream_t current_stream() { return nullptr; }
+void set_error(int, const char* what) { printf("error: %s\n", what); }
+}  // namespace bnb
 using namespace bnb;
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
-}
-
-// MODE 0: shared 256-entry pair LUT; MODE 1: no LUT (memory floor); MODE 2: 32 bank-private LUT copies
-// addressed by v_perm (byte*256 + lane4)
-template <int MODE, int R, int U, int NT, int THREADS>
-__global__ void __launch_bounds__(THREADS)
-k_lab(int M, int K, const uint16_t* __restrict__ A, const uint8_t* __restrict__ B, const float* __restrict__ absmax,
-      const float* __restrict__ datatype, uint16_t* __restrict__ out, int ldb, int bs_shift) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t gsm[];
-  constexpr int LUT_DW = (MODE == 2 || MODE == 5) ? 16384 : MODE == 6 ? 8192 : 256;
-  uint32_t* lut = gsm;
-  uint32_t* xs = gsm + LUT_DW;
-  constexpr int WPB = THREADS / 64;
-  const int lane = threadIdx.x & 63;
-  const int row0 = (blockIdx.x * WPB + (threadIdx.x >> 6)) * R;
-  const int nch = K >> 5;
-  const long long two_ldb = 2LL * ldb;
-  uint4 b[U][R];
-  float am[U][R];
-  typedef const __attribute__((address_space(1))) uint8_t* gbyte_p;
-  typedef const __attribute__((address_space(1))) float* gfloat_p;
-  typedef const __attribute__((address_space(1))) u32x4_t* gvec_p;
-  const uint8_t* Bq = B;
-  const float* Aq = absmax;
-  constexpr int NB = 2048 / THREADS;
-  uint32_t tv[NB];
-  if constexpr (MODE >= 3) {
-    // table first, then x by LDS-DMA (older than every weight load), then the weights
-    if constexpr (MODE == 3 || MODE == 4)
-      for (int i = threadIdx.x; i < 256; i += THREADS) lut[i] = pack_bf16x2(datatype[i >> 4], datatype[i & 15]);
-    if constexpr (MODE == 5 || MODE == 6)
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        const int e = (threadIdx.x + k * THREADS) >> 3;
-        tv[k] = pack_bf16x2(datatype[e >> 4], datatype[e & 15]);
-      }
-    const int nx = K >> 3, wave = threadIdx.x >> 6;
-    for (int j = 0; j * THREADS < nx; ++j) {
-      const int idx = (j * WPB + wave) * 64 + lane;
-      if (idx < nx) glds16(A + 8 * idx, reinterpret_cast<uint8_t*>(xs) + (j * WPB + wave) * 1024);
-    }
-    // launder the weight pointers so their loads stay between the DMA and the vmcnt wait below
-    uintptr_t bp = (uintptr_t)B, ap = (uintptr_t)absmax;
-    asm volatile("" : "+s"(bp), "+s"(ap)::"memory");
-    Bq = (const uint8_t*)bp;
-    Aq = (const float*)ap;
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int c = min(lane + 64 * u, nch - 1);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int row = min(row0 + r, M - 1);
-      if (NT) {
-        const u32x4_t v = __builtin_nontemporal_load((gvec_p)((gbyte_p)Bq + (long long)row * ldb + 16LL * c));
-        b[u][r] = make_uint4(v.x, v.y, v.z, v.w);
-      }
-      else b[u][r] = *reinterpret_cast<const uint4*>(Bq + (long long)row * ldb + 16LL * c);
-      am[u][r] = ((gfloat_p)Aq)[(two_ldb * row + 32LL * c) >> bs_shift];
-    }
-  }
-  if (MODE == 0) {
-    for (int i = threadIdx.x; i < 256; i += THREADS) lut[i] = pack_bf16x2(datatype[i >> 4], datatype[i & 15]);
-  } else if (MODE == 2) {
-    // entry e at dwords [64e, 64e+32): copy j in bank j
-    for (int i = threadIdx.x; i < 256 * 8; i += THREADS) {
-      const int e = i >> 3, q = i & 7;
-      const uint32_t v = pack_bf16x2(datatype[e >> 4], datatype[e & 15]);
-      reinterpret_cast<uint4*>(lut)[e * 16 + q] = make_uint4(v, v, v, v);
-    }
-  }
-  if constexpr (MODE == 5 || MODE == 6) {
-    // bank-private copies: entry e for lane-bank j at byte e*STRIDE + 4j (STRIDE 256 for v_perm addressing)
-    constexpr int STRIDE = MODE == 5 ? 256 : 128;
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      const int i = threadIdx.x + k * THREADS, e = i >> 3, q = i & 7;
-      *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(lut) + e * STRIDE + 16 * q) = make_uint4(tv[k], tv[k], tv[k], tv[k]);
-    }
-  }
-  if constexpr (MODE >= 3) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * R * U) : "memory");   // x landed; weights still in flight
-    __builtin_amdgcn_s_waitcnt(0xC07F);                                   // lgkmcnt(0): table writes
-    __builtin_amdgcn_s_barrier();
-  } else {
-    for (int i = threadIdx.x; i < (K >> 3); i += THREADS) reinterpret_cast<uint4*>(xs)[i] = reinterpret_cast<const uint4*>(A)[i];
-    __syncthreads();
-  }
-  if (row0 >= M) return;
-  float acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-  const uint32_t lane4 = (lane & 31) * 4;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const bool valid = lane + 64 * u < nch;
-    const int c = min(lane + 64 * u, nch - 1);
-    uint32_t x[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 v = reinterpret_cast<const uint4*>(xs + 16 * c)[q];
-      x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t w[4] = {b[u][r].x, b[u][r].y, b[u][r].z, b[u][r].w};
-      uint32_t l[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (MODE == 5) {
-          const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(i & 3)) << 8);
-          const uint32_t addr = __builtin_amdgcn_perm(w[i >> 2], lane4, sel);
-          l[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(lut) + addr);
-        } else if (MODE == 6) {
-          const uint32_t addr = (((w[i >> 2] >> (8 * (i & 3))) & 0xFF) << 7) | lane4;
-          l[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(lut) + addr);
-        } else if (MODE == 0 || MODE == 3) l[i] = lut[(w[i >> 2] >> (8 * (i & 3))) & 0xFF];
-        else if (MODE == 1 || MODE == 4) l[i] = w[i >> 2];
-        else {
-          // byte i&3 of w -> bits 8..15, lane4 -> bits 0..7
-          const uint32_t sel = 0x0C0C0000u | ((4u + (uint32_t)(i & 3)) << 8);   // src0 bytes are 4..7
-          const uint32_t addr = __builtin_amdgcn_perm(w[i >> 2], lane4, sel);
-          l[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(lut) + addr);
-        }
-      }
-      float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        s0 = dot2(x[i], l[i], s0);
-        s1 = dot2(x[i + 1], l[i + 1], s1);
-      }
-      const float part = (s0 + s1) * am[u][r];
-      acc[r] += valid ? part : 0.0f;
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
-  if (lane == 0) {
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (row0 + r < M) out[row0 + r] = (uint16_t)(__float_as_uint(acc[r]) >> 16);
-  }
-}
-
-template <int MODE> constexpr int LUTB() { return ((MODE == 2 || MODE == 5) ? 16384 : MODE == 6 ? 8192 : 256) * 4; }
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 int main() {
-  const int N = 11008, K = 4096, BS = 64, COPIES = 14, REPS = 20;
-  const size_t wbytes = (size_t)N * K / 2, nabs = (size_t)N * K / BS;
-  std::vector<uint8_t*> Bs(COPIES);
-  std::vector<float*> As(COPIES);
-  std::vector<uint8_t> hb(wbytes);
-  std::vector<float> ha(nabs);
-  srand(1);
-  for (auto& v : hb) v = rand() & 0xFF;
-  for (auto& v : ha) v = 0.01f + (rand() & 1023) / 1024.0f;
-  for (int i = 0; i < COPIES; ++i) {
-    CK(hipMalloc(&Bs[i], wbytes));
-    CK(hipMalloc(&As[i], nabs * 4));
-    CK(hipMemcpy(Bs[i], hb.data(), wbytes, hipMemcpyHostToDevice));
-    CK(hipMemcpy(As[i], ha.data(), nabs * 4, hipMemcpyHostToDevice));
-  }
-  uint16_t *x, *out;
+  const int M = 11008, K = 4096, BS = 64, COPIES = 14;
+  const size_t wbytes = (size_t)M * K / 2, nabs = (size_t)M * K / BS;
+  std::vector<uint8_t*> W(COPIES);
+  std::vector<float*> AM(COPIES);
+  bf16_t *x, *y0, *y1;
   float* code;
-  CK(hipMalloc(&x, K * 2));
-  CK(hipMalloc(&out, N * 2));
-  CK(hipMalloc(&code, 64));
-  std::vector<uint16_t> hx(K);
-  for (auto& v : hx) v = 0x3F80 ^ (rand() & 0x807F);
-  CK(hipMemcpy(x, hx.data(), K * 2, hipMemcpyHostToDevice));
-  float hc[16];
-  for (int i = 0; i < 16; ++i) hc[i] = (i - 7.5f) / 8.0f;
-  CK(hipMemcpy(code, hc, 64, hipMemcpyHostToDevice));
-  hipEvent_t e0, e1;
-  CK(hipEventCreate(&e0));
-  CK(hipEventCreate(&e1));
-  const double bytes = wbytes + nabs * 4.0 + K * 2 + N * 2;
-  auto run = [&](const char* name, auto kern, int R, int threads, size_t lds) {
-    const int waves = (N + R - 1) / R, wpb = threads / 64;
-    const int grid = (waves + wpb - 1) / wpb;
-    if (lds > 65536) CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    for (int i = 0; i < COPIES; ++i)
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, 0, N, K, x, Bs[i], As[i], code, out, K / 2, 6);
+  for (int c = 0; c < COPIES; ++c) { CK(hipMalloc(&W[c], wbytes)); CK(hipMalloc(&AM[c], nabs * 4)); }
+  CK(hipMalloc(&x, K * 2)); CK(hipMalloc(&y0, M * 2)); CK(hipMalloc(&y1, M * 2)); CK(hipMalloc(&code, 64));
+  {
+    std::vector<uint8_t> h(wbytes);
+    uint32_t r = 7;
+    for (auto& v : h) { r = r * 1664525u + 1013904223u; v = (uint8_t)(r >> 24); }
+    std::vector<float> a(nabs);
+    for (auto& v : a) { r = r * 1664525u + 1013904223u; v = 0.01f + (r >> 8) / 16777216.0f * 0.05f; }
+    for (int c = 0; c < COPIES; ++c) {
+      CK(hipMemcpy(W[c], h.data(), wbytes, hipMemcpyHostToDevice));
+      CK(hipMemcpy(AM[c], a.data(), nabs * 4, hipMemcpyHostToDevice));
+    }
+    std::vector<uint16_t> hx(K);
+    for (auto& v : hx) { r = r * 1664525u + 1013904223u; float f = ((r >> 8) / 16777216.0f - 0.5f); uint32_t u; memcpy(&u, &f, 4); v = (uint16_t)(u >> 16); }
+    CK(hipMemcpy(x, hx.data(), K * 2, hipMemcpyHostToDevice));
+    const float nf4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+                           -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
+                           0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+                           0.7229568362236023f, 1.0f};
+    CK(hipMemcpy(code, nf4, 64, hipMemcpyHostToDevice));
+  }
+  const size_t lds = GV_TABLE_BYTES + 2 * (size_t)K;
+  auto run = [&](const char* name, auto kern, int R, bf16_t* y, int reps) {
+    const int waves = (M + R - 1) / R;
+    const int grid = (waves + 3) / 4;
+    for (int i = 0; i < reps; ++i) {
+      const int c = i % COPIES;
+      GemvStats st{};
+      st.absmax = AM[c];
+      st.bs_shift = __builtin_ctz(BS);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, M, K, x, W[c], st, code, y, K / 2);
+    }
     CK(hipDeviceSynchronize());
-    CK(hipEventRecord(e0));
-    for (int r = 0; r < REPS; ++r)
-      for (int i = 0; i < COPIES; ++i)
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, 0, N, K, x, Bs[i], As[i], code, out, K / 2, 6);
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    float ms;
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    const double us = ms * 1e3 / (REPS * COPIES);
-    printf("%-34s %8.2f us  %7.0f GB/s\n", name, us, bytes / us / 1e3);
+    printf("%s done\n", name);
   };
-  const size_t xl = K * 2;
-#define RUN(MODE, R, U, NT, T) \
-  run("mode" #MODE " R" #R " U" #U " nt" #NT " T" #T, k_lab<MODE, R, U, NT, T>, R, T, (size_t)LUTB<MODE>() + xl)
-  RUN(3, 4, 2, 1, 256);
-  RUN(4, 4, 2, 1, 256);
-  RUN(5, 4, 2, 1, 512);
-  RUN(5, 8, 2, 1, 256);
-  RUN(5, 4, 2, 1, 256);
-  RUN(6, 4, 2, 1, 512);
-  RUN(6, 4, 2, 1, 256);
-  RUN(6, 2, 2, 1, 256);
+  auto check = [&](const char* name) {
+    std::vector<uint16_t> a(M), b(M);
+    CK(hipMemcpy(a.data(), y0, M * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), y1, M * 2, hipMemcpyDeviceToHost));
+    double md = 0, mr = 0;
+    for (int i = 0; i < M; ++i) {
+      uint32_t ua = (uint32_t)a[i] << 16, ub = (uint32_t)b[i] << 16;
+      float fa, fb; memcpy(&fa, &ua, 4); memcpy(&fb, &ub, 4);
+      md = std::max(md, (double)fabsf(fa - fb)); mr = std::max(mr, (double)fabsf(fa));
+    }
+    printf("  %s: max|d| %.4g of max|y| %.4g\n", name, md, mr);
+  };
+  for (int rep = 0; rep < 2; ++rep) {
+    run("R4U2 (library)", k_gemv_4bit_dot<bf16_t, 4, 2, false>, 4, y0, 200);
+    run("R2U4", k_gemv_4bit_dot<bf16_t, 2, 4, false>, 2, y1, 200); check("R2U4");
+    run("R8U1", k_gemv_4bit_dot<bf16_t, 8, 1, false>, 8, y1, 200); check("R8U1");
+    run("R4U4", k_gemv_4bit_dot<bf16_t, 4, 4, false>, 4, y1, 200); check("R4U4");
+    run("R8U2", k_gemv_4bit_dot<bf16_t, 8, 2, false>, 8, y1, 200); check("R8U2");
+    run("R2U8", k_gemv_4bit_dot<bf16_t, 2, 8, false>, 2, y1, 200); check("R2U8");
+  }
   return 0;
 }
