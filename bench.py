@@ -173,6 +173,56 @@ def bench_optimizer_8bit(dev, n=1 << 27, iters=10):
     return res
 
 
+def bench_nf4_fused_kernel(dev, m=M, n=N, k=K, iters=20):
+    """The hand-written fused NF4 GEMM (cgemm_4bit_inference_code_ws_bf16: dequantise in LDS + bf16
+    MFMA) at the metric shape, forced (functional.gemm_4bit routes this size to dequantise + hipBLASLt)."""
+    g = torch.Generator(device=dev).manual_seed(4)
+    X = torch.randn(m, k, device=dev, dtype=torch.bfloat16, generator=g)
+    W = (torch.randn(n, k, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True)
+    del W
+    Y = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    am = F._absmax_fp32(st)
+    saved = F.GEMM_4BIT_DEQUANT_MIN_ROWS
+    F.GEMM_4BIT_DEQUANT_MIN_ROWS = 1 << 30
+    try:
+        t = _time_loop(lambda: F.gemm_4bit(X, q, st, out=Y, absmax=am), iters)
+    finally:
+        F.GEMM_4BIT_DEQUANT_MIN_ROWS = saved
+    flops = 2.0 * m * n * k
+    return {"shape": [m, n, k], "kernel": "k_gemm_4bit_256<bf16>", "us": t * 1e6, "tflops": flops / t / 1e12,
+            "frac_of_bf16_peak": flops / t / 1e12 / PEAK_BF16_TFLOPS}
+
+
+def bench_llama2_7b_prefill(dev, batch=32, seq=2048, iters=3):
+    """Config 4: the seven Linear4bit NF4 projections of one Llama-2-7B decoder layer (q, k, v, o: 4096 ->
+    4096; gate, up: 4096 -> 11008; down: 11008 -> 4096; bs=64, nested statistics) at batch 32 x seq 2048
+    = 65,536 tokens, bf16, through functional.gemm_4bit (all 32 layers have these shapes; per-layer time)."""
+    tokens = batch * seq
+    hid, inter = 4096, 11008
+    g = torch.Generator(device=dev).manual_seed(6)
+    shapes = [(hid, hid)] * 4 + [(inter, hid)] * 2 + [(hid, inter)]
+    ws = []
+    for n_out, k_in in shapes:
+        W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        ws.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True))
+        del W
+    X = torch.randn(tokens, hid, device=dev, dtype=torch.bfloat16, generator=g)
+    Xi = torch.randn(tokens, inter, device=dev, dtype=torch.bfloat16, generator=g)
+    outs = {n_out: torch.empty(tokens, n_out, device=dev, dtype=torch.bfloat16) for n_out in (hid, inter)}
+
+    def layer():
+        for (n_out, k_in), (q, st) in zip(shapes, ws):
+            F.gemm_4bit(X if k_in == hid else Xi, q, st, out=outs[n_out])
+    t = _time_loop(layer, iters)
+    flops = sum(2.0 * tokens * n_out * k_in for n_out, k_in in shapes)
+    res = {"tokens": tokens, "layer_ms": t * 1e3, "tflops": flops / t / 1e12, "model_32_layers_ms": 32 * t * 1e3,
+           "path": gemm_kernel_name(tokens, hid)}
+    del X, Xi, outs, ws
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
     """Reference CPU path as ported (oracle/cpu_ops_port.cpp, the restated cpu_ops.cpp dequantize_cpu,
     single-threaded as written) + torch CPU F.linear (the CPU path has no GEMM), on a
@@ -224,7 +274,7 @@ def gemm_kernel_name(m, n, k=K):
     ks = max(1, F.lib.cgemm_4bit_workspace_bytes(ct.c_int32(n), ct.c_int32(m), ct.c_int32(k)) // (4 * m * n))
     tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
     tiles128 = ((m + 127) // 128) * ((n + 127) // 128)
-    if n >= 256 and 2 * tiles256 * ks >= tiles128:
+    if n >= 256 and (tiles256 * ks >= 128 or 2 * tiles256 * ks >= tiles128):
         return "k_gemm_4bit_256<bf16>" + (f" split-K x{ks} + k_splitk_reduce" if ks > 1 else "")
     return "k_gemm_4bit<bf16>"
 
@@ -350,6 +400,8 @@ def main():
         extras["decode_gemv_config2"] = bench_decode_gemv(dev)
         extras["dequant_nf4_config1_gpu"] = bench_dequant_config1(dev)
         extras["optimizer_adam8bit_blockwise"] = bench_optimizer_8bit(dev)
+        extras["nf4_fused_kernel_metric_shape"] = bench_nf4_fused_kernel(dev)
+        extras["llama2_7b_prefill_config4"] = bench_llama2_7b_prefill(dev)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.no_extras:
         try:

@@ -192,12 +192,13 @@ void gemm_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* a
   const bool pow2_bs = (blocksize & (blocksize - 1)) == 0;
   int ks = splitk_factor(m, n, k);
   if (ws == nullptr || ((uintptr_t)ws & 15) || (long long)ks * m * n * (long long)sizeof(float) > ws_bytes) ks = 1;
-  // 256x256 (with split-K) unless its grid is smaller than half the 128x128 grid, which then has more
-  // workgroups each running the full K (e.g. 512 features x 256 tokens: 8 workgroups of 128x128 took
-  // 174 us where 2 x 16-way split 256x256 tiles take ~25)
+  // 256x256 (with split-K) when its grid fills the chip (>= 128 workgroups), and also when it still has at
+  // least half the workgroups of the 128x128 grid, which then run the full K each (e.g. 512 features x
+  // 256 tokens: 8 workgroups of 128x128 took 174 us where 2 x 16-way split 256x256 tiles take ~25)
   const long long tiles128 = (long long)((m + G_BN - 1) / G_BN) * ((n + G_BM - 1) / G_BM);
   const bool use256 = pow2_bs && (g_tile_override == 256 ||
-                                  (g_tile_override != 128 && m >= 256 && 2 * tiles256 * ks >= tiles128));
+                                  (g_tile_override != 128 && m >= 256 &&
+                                   (tiles256 * ks >= 128 || 2 * tiles256 * ks >= tiles128)));
   if (use256) {
     launch_gemm_4bit_256<T>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, ws, ks);
   } else {
