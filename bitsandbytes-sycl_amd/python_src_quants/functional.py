@@ -562,15 +562,21 @@ def gemm_4bit_supported(A: Tensor, state: QuantState) -> bool:
 _GEMM_WS: dict = {}
 
 
+def _stream_key(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
 def _gemm_workspace(device, nbytes: int) -> Optional[Tensor]:
-    """Grow-only fp32 split-K workspace per device for gemm_4bit (cgemm_4bit_workspace_bytes); kept
-    across calls so steady-state calls (and HIP-graph replays) allocate nothing."""
+    """Grow-only fp32 split-K workspace per (device, stream) for gemm_4bit (cgemm_4bit_workspace_bytes);
+    kept across calls so steady-state calls (and HIP-graph replays) allocate nothing, and never shared
+    by two streams that could run GEMMs concurrently."""
     if nbytes <= 0:
         return None
-    ws = _GEMM_WS.get(device)
+    key = (device, _stream_key(device))
+    ws = _GEMM_WS.get(key)
     if ws is None or ws.numel() * 4 < nbytes:
         ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
-        _GEMM_WS[device] = ws
+        _GEMM_WS[key] = ws
     return ws
 
 
@@ -587,8 +593,9 @@ _DEQ_META: dict = {}
 
 
 def _dequant_workspace(device, dtype, numel: int) -> Tensor:
-    """Grow-only weight buffer per (device, dtype) for the dequantise + library-GEMM path."""
-    key = (device, dtype)
+    """Grow-only weight buffer per (device, dtype, stream) for the dequantise + library-GEMM path (the
+    size of the largest weight seen; per stream, so concurrent streams never share one)."""
+    key = (device, dtype, _stream_key(device))
     ws = _DEQ_WS.get(key)
     if ws is None or ws.numel() < numel:
         ws = torch.empty(numel, dtype=dtype, device=device)
@@ -629,7 +636,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         ev[0].record()
     if library:
         W = _dequant_workspace(A.device, A.dtype, N * K).view(N, K)
-        key = (A.device, A.dtype)
+        key = (A.device, A.dtype, _stream_key(A.device))
         stats = absmax if absmax is not None else state.absmax
         meta = (Bc.data_ptr(), Bc._version, stats.data_ptr(), stats._version, N, K, state.blocksize,
                 state.quant_type)

@@ -302,3 +302,26 @@ def test_gemm_4bit_reuse_weight_chunks(dev):
     q2, st2 = F.quantize_4bit(W2, blocksize=64, quant_type="nf4", compress_statistics=True)
     y2 = F.gemm_4bit(X[:2048], q2, st2, reuse_weight=True)
     assert torch.equal(y2, torch.matmul(X[:2048], F.dequantize_4bit(q2, st2).t()))
+
+
+def test_gemm_4bit_library_path_two_streams(dev):
+    """Two streams running the dequantise + library GEMM path concurrently on different weights each use
+    their own weight workspace (keyed by stream): both results equal their single-stream values."""
+    F = _F()
+    M, N, K = 2048, 2048, 1024
+    torch.manual_seed(29)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    qs = [F.quantize_4bit((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16), blocksize=64,
+                          quant_type="nf4", compress_statistics=True) for _ in range(2)]
+    ref_out = [F.gemm_4bit(X, q, st) for q, st in qs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    outs = [None, None]
+    for _ in range(3):
+        for i, s in enumerate(streams):
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                outs[i] = F.gemm_4bit(X, qs[i][0], qs[i][1])
+        torch.cuda.synchronize()
+        for i in range(2):
+            assert torch.equal(outs[i], ref_out[i])
