@@ -2,8 +2,8 @@
 // see gemm4bit.hip for the ABI / semantics; ref:sycl/pythonInterface.cpp:377-378, kernel_gemm.cpp:1015).
 //
 // Geometry: 512 threads = 8 waves (2 along tokens x 4 along out-features), 128 x 64 outputs per wave
-// (4 x 2 tiles of v_mfma_f32_32x32x16), BK = 64, one workgroup per CU (148 KiB LDS).  The 32x32x16
-// MFMA holds the SIMD's issue for 8 of its 32 cycles, so the dequantisation and DMA issue fit beside it.
+// (8 x 4 tiles of v_mfma_f32_16x16x32, or 4 x 2 of 32x32x16 with M16 = false), BK = 64, one workgroup
+// per CU (148 KiB LDS).
 //
 // Every operand arrives by LDS-DMA (global_load_lds), so no VGPR-destination load is ever in flight
 // in the k-loop (hipcc otherwise drains the prefetch early, cdna_hip_programming.md §5):
