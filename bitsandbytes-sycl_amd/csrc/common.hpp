@@ -212,8 +212,8 @@ __device__ __forceinline__ void quantize_dynamic8_n(Code code, const float (&x)[
 //    512  code[2L]                             at byte a    (the final pick's records share the offset
 //   1024  code[max(2L - 1, 0)]                 at a + 512    a of the search: immediate ds_read
 //   1536  code[2L + 1]                         at a + 1024   offsets, no address arithmetic)
-//   2048  (code[max(2L-1,0)] + code[2L]) * 0.5 at a + 1536   the two midpoints of quantize_dynamic8,
-//   2560  (code[2L+1] + code[2L]) * 0.5        at a + 2048   rounded as it rounds them
+//   2048  (code[2L-1] + code[2L]) * 0.5        at a + 1536   the two midpoints of quantize_dynamic8,
+//   2560  (code[2L+1] + code[2L]) * 0.5        at a + 2048   rounded as it rounds them (-inf at L = 0)
 //   3072  code[c], c = 0..255                  (dequantisation)
 constexpr int DYNMAP_FLOATS = 1024;
 
@@ -239,8 +239,8 @@ __device__ __forceinline__ void dynmap_stage(float* table, const float* __restri
       v = code[max(2 * L - 1, 0)];
     } else if (part == 3) {
       v = code[2 * L + 1];
-    } else if (part == 4) {
-      v = __fmul_rn(__fadd_rn(code[max(2 * L - 1, 0)], code[2 * L]), 0.5f);
+    } else if (part == 4) {   // -inf for p = 0: nothing lies below code[0]'s pick (q would clamp to 0)
+      v = L == 0 ? -__builtin_inff() : __fmul_rn(__fadd_rn(code[2 * L - 1], code[2 * L]), 0.5f);
     } else if (part == 5) {
       v = __fmul_rn(__fadd_rn(code[2 * L + 1], code[2 * L]), 0.5f);
     } else {
@@ -268,13 +268,13 @@ __device__ __forceinline__ void dynmap_quantize_n(DynMapView m, const float (&x)
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const float c = m.at(a[j]), mlo = m.at(a[j] + 1536), mhi = m.at(a[j] + 2048);
-    const bool up = x[j] > c;                    // quantize_dynamic8's tail, branch-free
-    const float th = up ? mhi : mlo;
-    const bool move = up ? (x[j] > th) : (x[j] < th);
+    // quantize_dynamic8's tail, branch-free: with mlo <= code[p] <= mhi (midpoints of a sorted map),
+    // "x > code[p] ? (x > mhi ? p+1 : p) : (x < mlo ? p-1 : p)" is p + (x > mhi) - (x < mlo)
+    const float mlo = m.at(a[j] + 1536), mhi = m.at(a[j] + 2048);
+    const bool up = x[j] > mhi, dn = x[j] < mlo;
     const int p = (a[j] - 512) >> 1;
-    q[j] = (uint32_t)max(p + (move ? (up ? 1 : -1) : 0), 0);
-    if constexpr (CQ) cq[j] = move ? (up ? m.at(a[j] + 1024) : m.at(a[j] + 512)) : c;
+    q[j] = (uint32_t)(p + (up ? 1 : 0) - (dn ? 1 : 0));
+    if constexpr (CQ) cq[j] = up ? m.at(a[j] + 1024) : (dn ? m.at(a[j] + 512) : m.at(a[j]));
   }
 }
 
