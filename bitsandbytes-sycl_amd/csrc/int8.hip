@@ -188,7 +188,7 @@ k_colrow_stats_wide(const fp16_t* __restrict__ A, float* __restrict__ rowStats, 
     raw[i] = (has_cols && row < rows) ? *reinterpret_cast<const uint4*>(A + (long long)row * cols + c0)
                                       : make_uint4(0, 0, 0, 0);
   }
-  float cmax[8];
+  float cmax[8], rmax[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) cmax[j] = -3.402823466e+38f;
 #pragma unroll
@@ -196,16 +196,44 @@ k_colrow_stats_wide(const fp16_t* __restrict__ A, float* __restrict__ rowStats, 
     const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
     const int row = base_row + wave + 4 * i;
     const bool ok = has_cols && row < rows;
-    float rmax = -3.402823466e+38f;
+    rmax[i] = -3.402823466e+38f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float v = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j >> 1] >> (16 * (j & 1))));
       const float a = ok ? fabsf(v) : -3.402823466e+38f;
       cmax[j] = fmaxf(cmax[j], a);
-      rmax = fmaxf(rmax, a);
+      rmax[i] = fmaxf(rmax[i], a);
     }
-    rmax = wave_max_xor(rmax, 64);
-    if (lane == 0 && row < rows && rmax >= 0.0f) atomic_max_nonneg(&rowStats[row], rmax);
+  }
+  // the 8 row maxima over the wave's 64 lanes by a halving butterfly: across lane bits 5, 4, 3 each lane
+  // keeps half of its rows (4 + 2 + 1 shuffles), then bits 0-2 reduce the one left (3) -- 10 shuffles
+  // instead of 8 full reductions (48); lane 8r' + 0 ends with row i = 4 b5 + 2 b4 + b3 of its lane id
+  {
+    const int h5 = (lane >> 5) & 1, h4 = (lane >> 4) & 1, h3 = (lane >> 3) & 1;
+    float r4[4], r2[2], r1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float send = h5 ? rmax[k] : rmax[k + 4];
+      const float mine = h5 ? rmax[k + 4] : rmax[k];
+      r4[k] = fmaxf(mine, __shfl_xor(send, 32, 64));
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float send = h4 ? r4[k] : r4[k + 2];
+      const float mine = h4 ? r4[k + 2] : r4[k];
+      r2[k] = fmaxf(mine, __shfl_xor(send, 16, 64));
+    }
+    {
+      const float send = h3 ? r2[0] : r2[1];
+      const float mine = h3 ? r2[1] : r2[0];
+      r1 = fmaxf(mine, __shfl_xor(send, 8, 64));
+    }
+    r1 = fmaxf(r1, __shfl_xor(r1, 1, 64));
+    r1 = fmaxf(r1, __shfl_xor(r1, 2, 64));
+    r1 = fmaxf(r1, __shfl_xor(r1, 4, 64));
+    const int i = 4 * h5 + 2 * h4 + h3;
+    const int row = base_row + wave + 4 * i;
+    if ((lane & 7) == 0 && row < rows && r1 >= 0.0f) atomic_max_nonneg(&rowStats[row], r1);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) s_col[wave][8 * lane + j] = cmax[j];
