@@ -74,10 +74,15 @@ def bench_int8(dev, m, n, k, iters=20):
         ca, _, sca, _, _ = F.double_quant(A)
         F.igemmlt_dequant(ca, CB, sca, SCB, out=out)
     t_fwd = _time_loop(fwd, max(5, iters // 2))
+
+    def fwd_inference():      # MatMul8bitLt without grad and outliers: one-pass row quantisation
+        ca, sca = F.int8_row_quant(A)
+        F.igemmlt_dequant(ca, CB, sca, SCB, out=out)
+    t_inf = _time_loop(fwd_inference, max(5, iters // 2))
     ops = 2.0 * m * n * k
     return {"shape": [m, n, k], "tops": ops / t_gemm / 1e12, "us": t_gemm * 1e6,
             "frac_of_int8_peak": ops / t_gemm / 1e12 / PEAK_INT8_TOPS,
-            "forward_with_double_quant_us": t_fwd * 1e6}
+            "forward_with_double_quant_us": t_fwd * 1e6, "forward_inference_row_quant_us": t_inf * 1e6}
 
 
 def _time_graph(calls, iters):

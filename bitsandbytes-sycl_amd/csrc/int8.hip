@@ -283,6 +283,58 @@ k_double_rowcol_quant_wide(const fp16_t* __restrict__ A, const float* __restrict
   }
 }
 
+// ============================================================================ one-pass row quantisation
+// The forward of LLM.int8 without outliers and without a backward needs only the row-normalised CA and
+// its row statistics (CAt / column stats serve the backward, autograd/_functions.py:436-483).  One wave
+// per row keeps the whole row in registers (cols <= 64 * 8 * RQ_MAX_VEC), so A is read once: the row
+// max (the row half of kgetColRowStats, kernel_quant.cpp:3214-3379) and the row quantisation (the row
+// half of kDoubleRowColQuant, 3384-3512) with the same expressions -- rowStats = max |a| (or the
+// -50000 the callers pre-fill when a row has no finite |a|), CA = rint(a * (127 / rowStats)).
+constexpr int RQ_MAX_VEC = 32;   // 16-B vectors per lane: K <= 16384
+
+__global__ void __launch_bounds__(256)
+k_row_quant(const fp16_t* __restrict__ A, float* __restrict__ rowStats, int8_t* __restrict__ out, int rows, int cols) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = cols >> 3;
+  const uint4* src = reinterpret_cast<const uint4*>(A + (long long)row * cols);
+  uint4 v[RQ_MAX_VEC];
+#pragma unroll
+  for (int i = 0; i < RQ_MAX_VEC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nvec) v[i] = src[c];
+  }
+  float m = -3.402823466e+38f;
+#pragma unroll
+  for (int i = 0; i < RQ_MAX_VEC; ++i) {
+    if (lane + 64 * i < nvec) {
+      const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j >> 1] >> (16 * (j & 1))))));
+    }
+  }
+  m = wave_max_xor(m, 64);
+  if (!(m >= 0.0f)) m = -50000.0f;               // the callers' pre-fill, untouched by atomicMax
+  if (lane == 0) rowStats[row] = m;
+  const float rsc = __fdiv_rn(127.0f, m);
+  uint2* dst = reinterpret_cast<uint2*>(out + (long long)row * cols);
+#pragma unroll
+  for (int i = 0; i < RQ_MAX_VEC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nvec) {
+      const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+      uint32_t q[2] = {0, 0};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j >> 1] >> (16 * (j & 1))));
+        q[j >> 2] |= (uint32_t)(uint8_t)rint_i8(__fmul_rn(a, rsc)) << (8 * (j & 3));
+      }
+      dst[c] = make_uint2(q[0], q[1]);
+    }
+  }
+}
+
 // ============================================================================ layout transforms
 // One thread per element (row-major source index i).  These are load-time / small-tensor ops.
 
@@ -535,6 +587,17 @@ void cget_col_row_stats(fp16_t* A, float* rowStats, float* colStats, int* nnz_co
     hipLaunchKernelGGL(k_colrow_stats<false>, dim3(row_tiles * col_tiles), dim3(256), 0, current_stream(), A, rowStats,
                        colStats, nnz_count_row, nnz_threshold, rows, cols, col_tiles, vec);
   BNB_LAUNCH_CHECK("get_col_row_stats");
+}
+
+// [additive] CA and row statistics in one pass (the row halves of cget_col_row_stats + cdouble_rowcol_quant,
+// threshold 0).  Returns 0 when launched, 1 when the shape needs the two-kernel path.
+int cint8_row_quant_fp16(fp16_t* A, float* rowStats, char* out_row, int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (cols % 8 || cols > 64 * 8 * RQ_MAX_VEC || ((uintptr_t)A & 15) || ((uintptr_t)out_row & 7)) return 1;
+  hipLaunchKernelGGL(k_row_quant, dim3((rows + 3) / 4), dim3(256), 0, current_stream(), A, rowStats, (int8_t*)out_row,
+                     rows, cols);
+  BNB_LAUNCH_CHECK("int8_row_quant");
+  return 0;
 }
 
 void cdouble_rowcol_quant(fp16_t* A, float* rowStats, float* colStats, char* out_col_normed, char* out_row_normed,

@@ -70,8 +70,13 @@ class MatMul8bitLt(torch.autograd.Function):
             warnings.warn(f"MatMul8bitLt: inputs will be cast from {A.dtype} to float16 during quantization")
         if len(A.shape) == 3:
             A = A.reshape(-1, A.shape[-1])
-        # 1. quantise A (row- and column-normalised)
-        CA, CAt, SCA, SCAt, coo_tensorA = F.double_quant(A.to(torch.float16), threshold=state.threshold)
+        # 1. quantise A (row- and column-normalised; only the row half, in one pass over A, when there are
+        #    no outliers to split off and no backward will read CAt)
+        if state.threshold == 0.0 and not any(ctx.needs_input_grad[:2]):
+            CA, SCA = F.int8_row_quant(A.to(torch.float16))
+            CAt, SCAt, coo_tensorA = None, None, None
+        else:
+            CA, CAt, SCA, SCAt, coo_tensorA = F.double_quant(A.to(torch.float16), threshold=state.threshold)
         subA = None
         if state.threshold > 0.0 and coo_tensorA is not None and state.has_fp16_weights:
             idx = torch.unique(coo_tensorA.colidx).long()

@@ -41,7 +41,8 @@ class BNBNativeLibrary:
                      "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cget_last_error", "cget_abi_version",
                      "cgemm_4bit_inference_naive_nested_fp16", "cgemm_4bit_inference_naive_nested_bf16",
                      "cdequantize_blockwise_nested_fp16_fp4", "cdequantize_blockwise_nested_fp16_nf4",
-                     "cdequantize_blockwise_nested_bf16_fp4", "cdequantize_blockwise_nested_bf16_nf4"):
+                     "cdequantize_blockwise_nested_bf16_fp4", "cdequantize_blockwise_nested_bf16_nf4",
+                     "cint8_row_quant_fp16"):
             getattr(lib, name).restype = ct.c_int
 
     def __getattr__(self, item):

@@ -995,6 +995,27 @@ def spmm_coo_very_sparse(cooA: COOSparseTensor, B: Tensor, dequant_stats: Option
     return out
 
 
+def int8_row_quant(A: Tensor, out_row: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """(CA, row_stats) of double_quant(A) with threshold 0 -- the row-normalised int8 matrix and its fp32
+    row absmax -- in one pass over A (cint8_row_quant_fp16); what the LLM.int8 forward needs when no
+    backward will use CAt.  Falls back to double_quant for shapes the one-pass kernel does not take."""
+    assert A.dtype == torch.half and A.device.type == "cuda"
+    rows = A.numel() // A.shape[-1]
+    cols = A.shape[-1]
+    A2 = A if A.is_contiguous() else A.contiguous()
+    if out_row is None:
+        out_row = torch.empty(A.shape, device=A.device, dtype=torch.int8)
+    row_stats = torch.empty((rows,), device=A.device, dtype=torch.float32)
+    prev_device = pre_call(A.device)
+    is_on_gpu([A2, row_stats, out_row])
+    rc = lib.cint8_row_quant_fp16(get_ptr(A2), get_ptr(row_stats), get_ptr(out_row), ct.c_int32(rows), ct.c_int32(cols))
+    post_call(prev_device)
+    if rc != 0:
+        CA, _, SCA, _, _ = double_quant(A2, out_row=out_row)
+        return CA, SCA
+    return out_row, row_stats
+
+
 def extract_outliers(A, SA, idx):
     """Gather int8 columns `idx` of a turing/ampere-tiled matrix (ref:functional.py:2914-2936)."""
     shapeA, formatA = SA[0], SA[1]

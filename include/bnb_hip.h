@@ -110,6 +110,10 @@ void cgemm_4bit_set_tile(int tile);
 /* ---- LLM.int8 statistics and quantisation: ref:sycl/pythonInterface.cpp:333-339 ---- */
 void cget_col_row_stats(bnb_fp16* A, float* rowStats, float* colStats, int* nnz_count_row, float nnz_threshold, int rows,
                         int cols);                                                               /* :335 */
+/* [additive] CA and row statistics of cdouble_rowcol_quant (threshold 0) in one pass over A, for the
+ * inference forward (no CAt needed).  Returns 0 when launched, 1 when the shape needs the two-kernel path
+ * (cols % 8, cols > 16384, unaligned pointers). */
+int cint8_row_quant_fp16(bnb_fp16* A, float* rowStats, char* out_row, int rows, int cols);
 void cdouble_rowcol_quant(bnb_fp16* A, float* rowStats, float* colStats, char* out_col_normed, char* out_row_normed,
                           int* rowidx, int* colidx, bnb_fp16* val, int* nnz_row_ptr, float threshold, int rows,
                           int cols);                                                             /* :338 */

@@ -176,3 +176,36 @@ def test_extract_outliers(dev):
         CxB, SB = F.transform(torch.from_numpy(B).to(dev), fmt)
         out = F.extract_outliers(CxB, SB, idx)
         assert np.array_equal(out.cpu().numpy(), B[:, idx.cpu().numpy()])
+
+
+@pytest.mark.parametrize("shape", [(4096, 11008), (33, 520), (7, 16384), (5, 16392), (3, 8), (300, 1030)])
+def test_int8_row_quant_matches_double_quant(dev, shape):
+    """The one-pass row quantisation (inference forward) gives double_quant's CA and row stats bit for bit,
+    including a zero row and an all-NaN row (row stat stays at the -50000 pre-fill)."""
+    F = _F()
+    torch.manual_seed(shape[1])
+    A = (torch.randn(*shape, device=dev) * 3).half()
+    A[0] = 0
+    if shape[0] > 2:
+        A[2] = float("nan")
+    CA, SCA = F.int8_row_quant(A)
+    orow, _, rs, _, _ = F.double_quant(A)
+    assert same_bits(SCA.cpu().numpy(), rs.cpu().numpy())
+    assert same_bits(CA.cpu().numpy(), orow.cpu().numpy())
+
+
+def test_matmul8bitlt_inference_uses_row_quant(dev):
+    """Linear8bitLt-style inference (no grad, threshold 0) through the one-pass quantisation equals the
+    double_quant route (same CA, same fused GEMM)."""
+    F = _F()
+    from python_src_quants.autograd._functions import MatMul8bitLt, MatmulLtState
+    torch.manual_seed(8)
+    A = torch.randn(64, 512, device=dev).half()
+    W = (torch.randn(256, 512, device=dev) * 0.05).half()
+    st = MatmulLtState()
+    st.has_fp16_weights = False
+    st.CB, _, st.SCB, _, _ = F.double_quant(W)
+    out = MatMul8bitLt.apply(A, W, None, None, st)
+    CA, _, SCA, _, _ = F.double_quant(A)
+    exp = F.igemmlt_dequant(CA, st.CB, SCA, st.SCB)
+    assert torch.equal(out, exp)
