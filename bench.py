@@ -417,8 +417,10 @@ def main():
     if rank == 0:
         pmc = load_pmc_traffic()
         traffic = None
+        pmc_extra = {}
         if pmc and pmc.get("kernel") == gemm_kernel_name(Mc, shard) and pmc.get("shape") == [Mc, shard, K]:
             traffic = pmc.get("hbm_bytes_per_launch")
+            pmc_extra = {k: pmc[k] for k in ("mfma_busy_per_simd", "effective_clock_ghz") if k in pmc}
         line = {
             "metric": "NF4 matmul TFLOPS + INT8 igemmlt TOPS @ 4096x4096x11008, 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -442,7 +444,7 @@ def main():
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                          "kernel": gemm_kernel_name(Mc, shard), "kernel_us": round(kern_s * 1e6, 2),
                          "flops_per_launch": shard_flops,
-                         "dequantize_us": round(deq_s * 1e6, 2) if deq_s else None},
+                         "dequantize_us": round(deq_s * 1e6, 2) if deq_s else None, **pmc_extra},
             "cpu_baseline": cpu,
         }
         line.update(extras)
