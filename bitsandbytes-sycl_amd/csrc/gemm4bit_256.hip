@@ -32,7 +32,10 @@ constexpr int Q_OFF_W = 2 * Q_XT;
 constexpr int Q_OFF_P = Q_OFF_W + 2 * Q_WT;
 constexpr int Q_OFF_A = Q_OFF_P + 2 * Q_PT;
 constexpr int Q_OFF_L = Q_OFF_A + 2 * Q_AT;
-constexpr int Q_LDS = Q_OFF_L + 256 * 8;       // 151,552 B
+// the byte -> {code[hi], code[lo]} LUT as Q_LUTC interleaved copies (entry b of copy j at b * Q_LUTC + j,
+// lane l reads copy l % Q_LUTC): random-byte ds_read_b64 lookups of one copy serialise on bank conflicts
+constexpr int Q_LUTC = 4;
+constexpr int Q_LDS = Q_OFF_L + 256 * 8 * Q_LUTC;   // 157,696 B
 constexpr int Q_EPI_STRIDE = 136;              // staged output row: 128 B + 8 B pad
 static_assert(8 * 128 * Q_EPI_STRIDE <= Q_OFF_L, "epilogue staging must not overlap the LUT");
 
@@ -61,7 +64,7 @@ template <> __device__ __forceinline__ uint32_t cvt2<fp16_t>(float lo, float hi)
 // load (MI355X_MICROARCH.md 'DVFS give-back' item 7): 326 vs 346 us at 4096 x 4096 x 11008, bit-identical
 // outputs (tools/gemm_m16_lab.hip).  The fragment reads (rows l & 15, slot 4 s + (l >> 4)) stay
 // conflict-free under the (row >> 1) & 7 swizzle.
-template <typename T, bool SPLIT, bool M16 = false>
+template <typename T, bool SPLIT, bool M16 = false, int LUTC = Q_LUTC>
 __global__ void __launch_bounds__(Q_THREADS, 1)
 k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B,
                 const float* __restrict__ absmax, const float* __restrict__ datatype, T* __restrict__ out,
@@ -69,9 +72,10 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
   const int ksplit = SPLIT ? ksplit_arg : 1;    // the unsplit instance keeps the k-loop free of split terms
   __shared__ __attribute__((aligned(16))) uint8_t smem[Q_LDS];
   float2* lut = reinterpret_cast<float2*>(smem + Q_OFF_L);
+  const float2* lutc = lut + (threadIdx.x & (LUTC - 1));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);        // provably wave-uniform (SGPR math)
-  if (tid < 256) lut[tid] = make_float2(datatype[tid >> 4], datatype[tid & 15]);
+  for (int e = tid; e < 256 * LUTC; e += Q_THREADS) lut[e] = make_float2(datatype[(e / LUTC) >> 4], datatype[(e / LUTC) & 15]);
 
   // ---- tile order: XCD-contiguous ids, grouped 4 token-tiles x all feature-tiles; with split-K
   // (ksplit > 1) the split is the outer index, so an XCD's workgroups share one K range
@@ -120,7 +124,7 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
   const int dhalf = (g >> 4) & 1;
   auto lut_reads = [&](uint32_t word, float2 (&c)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) c[j] = lut[(word >> (8 * j)) & 0xFF];
+    for (int j = 0; j < 4; ++j) c[j] = lutc[((word >> (8 * j)) & 0xFF) * LUTC];
   };
   auto finish = [&](const float2 (&c)[4], float am, uint8_t* ws, int q) {   // 4 bytes -> one 16-B slot
     uint32_t pk[4];

@@ -32,8 +32,9 @@ int main(int argc, char** argv) {
   }
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  auto l32 = [&]() { hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t, false, false>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y0, K, K / 2, N, BS, (float*)nullptr, 1); };
-  auto l16 = [&]() { hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t, false, true>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y1, K, K / 2, N, BS, (float*)nullptr, 1); };
+  auto l32 = [&]() { hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t, false, false, 1>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y0, K, K / 2, N, BS, (float*)nullptr, 1); };
+  auto l16 = [&]() { hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t, false, true, 1>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y1, K, K / 2, N, BS, (float*)nullptr, 1); };
+  auto l16c = [&]() { hipLaunchKernelGGL((k_gemm_4bit_256<bf16_t, false, true, 4>), dim3(tiles), dim3(512), 0, 0, N, M, K, (const bf16_t*)X, W, am, code, (bf16_t*)Y1, K, K / 2, N, BS, (float*)nullptr, 1); };
   for (int i = 0; i < 200; ++i) { l32(); l16(); }
   CK(hipDeviceSynchronize());
   {
@@ -49,15 +50,25 @@ int main(int argc, char** argv) {
     printf("agreement: max|d| %.4g  max|y| %.4g  outside tol %zu / %zu\n", md, mr, bad, a.size());
   }
   const double flop = 2.0 * M * N * K;
+  for (int i = 0; i < 50; ++i) l16c();
+  CK(hipDeviceSynchronize());
+  {
+    std::vector<uint16_t> a((size_t)M * N), b((size_t)M * N);
+    CK(hipMemcpy(a.data(), Y0, a.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), Y1, b.size() * 2, hipMemcpyDeviceToHost));
+    printf("LUT x4 vs 32x32: %s\n", memcmp(a.data(), b.data(), a.size() * 2) ? "DIFFER" : "bit-identical");
+  }
+  const char* names[3] = {"32x32x16 LUTx1", "16x16x32 LUTx1", "16x16x32 LUTx4"};
   for (int rep = 0; rep < 4; ++rep) {
-    for (int which = 0; which < 2; ++which) {
-      for (int i = 0; i < 20; ++i) { if (which) l16(); else l32(); }
+    for (int which = 0; which < 3; ++which) {
+      auto go = [&]() { if (which == 0) l32(); else if (which == 1) l16(); else l16c(); };
+      for (int i = 0; i < 20; ++i) go();
       CK(hipEventRecord(e0));
-      for (int i = 0; i < 30; ++i) { if (which) l16(); else l32(); }
+      for (int i = 0; i < 30; ++i) go();
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       const double us = ms * 1e3 / 30;
-      printf("%s %8.1f us  %7.1f TFLOP/s\n", which ? "16x16x32" : "32x32x16", us, flop / us / 1e6);
+      printf("%s %8.1f us  %7.1f TFLOP/s\n", names[which], us, flop / us / 1e6);
     }
   }
   return 0;
