@@ -175,6 +175,23 @@ def bench_optimizer_8bit(dev, n=1 << 27, iters=10):
         res[name] = {"us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS,
                      "bytes": nbytes}
         del p, grad, s1, s2
+    # the fp32-state Adam (c<T>adam32bit_grad) on the same parameters: g + p read, p write, two fp32 states
+    # read + written -- pure streaming, the HBM reference point for the 8-bit kernels above
+    g = torch.Generator(device=dev).manual_seed(9)
+    p = (torch.randn(n, device=dev, generator=g) * 0.1)
+    grad = (torch.randn(n, device=dev, generator=g) * 0.01)
+    s1 = torch.zeros(n, device=dev)
+    s2 = torch.zeros(n, device=dev)
+    step = [0]
+
+    def call32():
+        step[0] += 1
+        F.optimizer_update_32bit("adam", grad, p, s1, 0.9, 1e-8, step[0], 1e-3, state2=s2, beta2=0.999)
+    t = _time_loop(call32, iters)
+    nbytes = n * 28
+    res["fp32_states_fp32"] = {"us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS,
+                               "bytes": nbytes}
+    del p, grad, s1, s2
     return res
 
 
