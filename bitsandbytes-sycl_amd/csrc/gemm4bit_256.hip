@@ -186,8 +186,8 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
     if constexpr (M16) {
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
-        dma_x_piece(min(t + 1, nk - 1), s ^ 1, 2 * k2);
-        dma_x_piece(min(t + 1, nk - 1), s ^ 1, 2 * k2 + 1);
+        dma_x_piece(min(t + 1, nk - 1), s ^ 1, 2 * k2);   // spread over the sub-steps (all at the top of
+        dma_x_piece(min(t + 1, nk - 1), s ^ 1, 2 * k2 + 1);   // the step measured 3 % slower)
         if (k2 == 0) dma_w(min(t + 2, nk - 1), s);
         const int slot = 4 * k2 + (lane >> 4);
         uint4 a[8], b[4];
