@@ -3,7 +3,8 @@
 // igemmlt + dequant_mm_int32_fp16 path (ref:sycl/sycl_code/kernel_quant.cpp:3846-3987).
 //
 // Geometry: 512 threads = 8 waves (2 along M x 4 along N), 128 x 64 outputs per wave (8 x 4 tiles of
-// 16x16), BK = 128 bytes, two LDS stages (2 x (32 + 32) KiB), one barrier per k-step.  Both operands
+// 16x16), BK = 128 bytes, two LDS stages (2 x (32 + 32) KiB), one barrier per k-step, fragments register-
+// pipelined across it.  Both operands
 // arrive by LDS-DMA (16 B per lane, XOR-swizzled through the source address) from any layout whose
 // 16-k runs are contiguous: row-major, col32 (A) and col_ampere (B).  Fragment convention: lane l
 // holds 16 consecutive k of row l&15, k-chunk l>>4 -- identical for A and B, so the int32 result is
@@ -73,33 +74,50 @@ k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __r
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = i32x4_t{0, 0, 0, 0};
 
+  // Cross-barrier pipeline: tile t's ks = 1 fragments are read into registers before its ks = 0 MFMAs,
+  // so after the barrier the wave reads tile t+1's ks = 0 fragments under tile t's ks = 1 MFMAs; the
+  // barrier and a tile's first LDS latency hide behind 32 MFMAs (tools/igemm_lab.hip: 5-8 % over
+  // reading each k-half after the barrier, outputs bit-identical).
+  uint4 fa[2][8], fb[2][4];
+  auto frag = [&](int buf, int ks, uint4 (&a)[8], uint4 (&b)[4]) {
+    const uint8_t* as = smem + buf * J_TILE;
+    const uint8_t* bs = smem + 2 * J_TILE + buf * J_TILE;
+    const int slot = 4 * ks + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz(64 * wn + 16 * j + (lane & 15), slot));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const uint4*>(as + swz(128 * wm + 16 * i + (lane & 15), slot));
+  };
+  auto mma = [&](const uint4 (&a)[8], const uint4 (&b)[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a[i]), __builtin_bit_cast(i32x4_t, b[j]),
+                                                          acc[i][j], 0, 0, 0);
+  };
   const int nk = K / J_BK;
   dma(0, 0);
-  wait_vmcnt0();
+  if (nk > 1) {
+    dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed; tile 1 stays in flight
+  } else {
+    wait_vmcnt0();
+  }
   __syncthreads();
+  frag(0, 0, fa[0], fb[0]);
   for (int t = 0; t < nk; ++t) {
     const int s = t & 1;
-    dma(min(t + 1, nk - 1), s ^ 1);
-    const uint8_t* as = smem + s * J_TILE;
-    const uint8_t* bs = smem + 2 * J_TILE + s * J_TILE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int slot = 4 * ks + (lane >> 4);
-      uint4 b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz(64 * wn + 16 * j + (lane & 15), slot));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint4 a = *reinterpret_cast<const uint4*>(as + swz(128 * wm + 16 * i + (lane & 15), slot));
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a), __builtin_bit_cast(i32x4_t, b[j]),
-                                                            acc[i][j], 0, 0, 0);
-      }
-    }
-    wait_vmcnt0();
-    __syncthreads();
+    frag(s, 1, fa[1], fb[1]);
+    mma(fa[0], fb[0]);
+    wait_vmcnt0();                                     // this wave's part of tile t+1 landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // and its reads of tile t are done
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) dma(t + 2, s);                     // every wave is past tile t: reuse its stage
+    if (t + 1 < nk) frag(s ^ 1, 0, fa[0], fb[0]);
+    mma(fa[1], fb[1]);
   }
+  __syncthreads();                                     // epilogue staging reuses the stages
 
   // ---- epilogues (C/D: col = lane&15, row = 4*(lane>>4) + r)
   const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;

@@ -1,11 +1,14 @@
-// int8 GEMM design lab: the library's 256x256 kernel (csrc/igemm_256.hip: BK = 128, 2 LDS stages,
-// vmcnt(0) + __syncthreads per k-step) against a 3-stage variant (BK = 64 bytes, DMA two tiles ahead,
+// int8 GEMM design lab: the library's 256x256 kernel (csrc/igemm_256.hip: BK = 128, 2 LDS stages, one
+// barrier per k-step, fragments pipelined across it -- the 'cross-barrier' variant below, adopted) against
+// a 3-stage variant (BK = 64 bytes, DMA two tiles ahead,
 // counted vmcnt, raw s_barrier) on the fused igemmlt + mm_dequant path, row-major A [M,K], B [N,K].
 // Outputs must be bit-identical (exact int32 + the same epilogue).  Usage: igemm_lab [M N K]
 #include "igemm_256.hip"
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
+#include <functional>
 
 namespace bnb {
 hipStream_t current_stream() { return nullptr; }
@@ -128,6 +131,127 @@ k_igemm_3s(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __re
     *reinterpret_cast<uint4*>(out + (long long)grow * ldc + gcol) = make_uint4(lo.x, lo.y, hi.x, hi.y);
   }
 }
+
+// Cross-barrier pipeline on the library geometry (BK = 128, 2 stages): the ks = 1 fragments are read
+// into registers before the ks = 0 MFMAs, so after the barrier the wave reads tile t+1's ks = 0
+// fragments while it runs tile t's ks = 1 MFMAs -- the barrier and the first LDS latency of a tile
+// are covered by 32 MFMAs instead of exposed.
+template <int FL>
+__global__ void __launch_bounds__(J_THREADS, 1)
+k_igemm_xb(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restrict__ B, fp16_t* __restrict__ out,
+           long long lda, long long ldb, long long ldc, const float* __restrict__ rowStats,
+           const float* __restrict__ colStats, const fp16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[J_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (N + 255) / 256, tilesM = (M + 255) / 256;
+  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  constexpr int GROUP = 4;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int8_t* asrc[4];
+  const int8_t* bsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wave + i) + (lane >> 3);
+    const int ks = 16 * ((lane & 7) ^ (row & 7));
+    asrc[i] = A + (long long)min(m0 + row, M - 1) * lda + ks;
+    bsrc[i] = B + (long long)min(n0 + row, N - 1) * ldb + ks;
+  }
+  auto dma = [&](int kt, int buf) {
+    const long long k0 = (long long)kt * J_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(asrc[i] + k0, smem + buf * J_TILE + (4 * wave + i) * 1024);
+      glds16(bsrc[i] + k0, smem + 2 * J_TILE + buf * J_TILE + (4 * wave + i) * 1024);
+    }
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  i32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = i32x4_t{0, 0, 0, 0};
+  uint4 fa[2][8], fb[2][4];
+  auto frag = [&](int buf, int ks, uint4 (&a)[8], uint4 (&b)[4]) {
+    const uint8_t* as = smem + buf * J_TILE;
+    const uint8_t* bs = smem + 2 * J_TILE + buf * J_TILE;
+    const int slot = 4 * ks + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz(64 * wn + 16 * j + (lane & 15), slot));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const uint4*>(as + swz(128 * wm + 16 * i + (lane & 15), slot));
+  };
+  auto mma = [&](const uint4 (&a)[8], const uint4 (&b)[4]) {
+    if (FL & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a[i]), __builtin_bit_cast(i32x4_t, b[j]),
+                                                          acc[i][j], 0, 0, 0);
+    if (FL & 1) __builtin_amdgcn_s_setprio(0);
+  };
+  const int nk = K / J_BK;
+  dma(0, 0);
+  if (nk > 1) dma(1, 1);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else wait_vmcnt0();
+  __syncthreads();
+  frag(0, 0, fa[0], fb[0]);
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    frag(s, 1, fa[1], fb[1]);
+    mma(fa[0], fb[0]);
+    if (FL & 2) __builtin_amdgcn_sched_barrier(0);      // keep the ks = 0 MFMAs ahead of the barrier
+    wait_vmcnt0();                                     // tile t+1 landed (this wave's part)
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // this wave's reads of tile t are done
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) dma(t + 2, s);
+    if (t + 1 < nk) frag(s ^ 1, 0, fa[0], fb[0]);
+    if (FL & 4) __builtin_amdgcn_sched_barrier(0);      // reads issued before the ks = 1 MFMAs
+    mma(fa[1], fb[1]);
+    if (FL & 2) __builtin_amdgcn_sched_barrier(0);
+  }
+  wait_vmcnt0();
+  __syncthreads();
+
+  const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;
+  uint8_t* ep = smem + wave * (128 * J_EPI_STRIDE);
+  float cs[4], bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = min(gcol0 + 16 * j + (lane & 15), N - 1);
+    cs[j] = colStats[col];
+    bv[j] = bias ? (float)bias[col] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * i + 4 * (lane >> 4) + r;
+      const float rs = rowStats[min(grow0 + row, M - 1)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<fp16_t*>(ep + row * J_EPI_STRIDE + 2 * (16 * j + (lane & 15))) =
+            mm_dequant_value(acc[i][j][r], rs, cs[j], bv[j]);
+    }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = lane + 64 * it;
+    const int row = id >> 3, c8 = id & 7;
+    const int grow = grow0 + row, gcol = gcol0 + 8 * c8;
+    if (grow >= M || gcol + 8 > N) continue;
+    const uint2 lo = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8);
+    const uint2 hi = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8 + 8);
+    *reinterpret_cast<uint4*>(out + (long long)grow * ldc + gcol) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
 }  // namespace bnb
 using namespace bnb;
 
@@ -170,7 +294,7 @@ int main(int argc, char** argv) {
     printf("%-22s %8.1f us  %7.1f TOPS\n", name, us, 2.0 * M * N * K / us / 1e6);
     fflush(stdout);
   };
-  for (int i = 0; i < 300; ++i) lib();
+  for (int i = 0; i < 100; ++i) lib();
   CK(hipDeviceSynchronize());
   auto check = [&]() {
     std::vector<uint16_t> a((size_t)M * N), b((size_t)M * N);
@@ -180,12 +304,28 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < a.size(); ++i) diff += a[i] != b[i];
     printf("  bit-identical: %s (%zu differ)\n", diff ? "NO" : "yes", diff);
   };
-  for (int rep = 0; rep < 2; ++rep) {
-    time("lib 256 BK128 2-stage", lib);
-    time("3-stage BK64", v3(k_igemm_3s<0>));
-    check();
-    time("3-stage BK64 setprio", v3(k_igemm_3s<1>));
-    check();
+  // correctness once, then interleaved timing (clock under load drifts; alternate the variants)
+  struct V { const char* name; std::function<void()> fn; std::vector<double> us; };
+  std::vector<V> vs;
+  vs.push_back({"lib 256 BK128 2-stage", lib, {}});
+  vs.push_back({"3-stage BK64", v3(k_igemm_3s<0>), {}});
+  vs.push_back({"cross-barrier", v3(k_igemm_xb<0>), {}});
+  vs.push_back({"xb sched_barrier", v3(k_igemm_xb<2>), {}});
+  vs.push_back({"xb sched_barrier x2", v3(k_igemm_xb<6>), {}});
+  for (size_t v = 1; v < vs.size(); ++v) { vs[v].fn(); CK(hipDeviceSynchronize()); printf("%s", vs[v].name); check(); }
+  for (int rep = 0; rep < 12; ++rep)
+    for (auto& v : vs) {
+      for (int i = 0; i < 2; ++i) v.fn();
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 10; ++i) v.fn();
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1e3 / 10);
+    }
+  for (auto& v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    const double med = v.us[v.us.size() / 2];
+    printf("%-24s median %7.1f us  min %7.1f  max %7.1f  %7.1f TOPS\n", v.name, med, v.us.front(), v.us.back(), 2.0 * M * N * K / med / 1e6);
   }
   return 0;
 }
