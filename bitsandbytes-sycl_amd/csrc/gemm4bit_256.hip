@@ -64,7 +64,7 @@ template <> __device__ __forceinline__ uint32_t cvt2<fp16_t>(float lo, float hi)
 // load (MI355X_MICROARCH.md 'DVFS give-back' item 7): 326 vs 346 us at 4096 x 4096 x 11008, bit-identical
 // outputs (tools/gemm_m16_lab.hip).  The fragment reads (rows l & 15, slot 4 s + (l >> 4)) stay
 // conflict-free under the (row >> 1) & 7 swizzle.
-template <typename T, bool SPLIT, bool M16 = false, int LUTC = Q_LUTC>
+template <typename T, bool SPLIT, bool M16 = false, int LUTC = Q_LUTC, bool XB = false>
 __global__ void __launch_bounds__(Q_THREADS, 1)
 k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B,
                 const float* __restrict__ absmax, const float* __restrict__ datatype, T* __restrict__ out,
@@ -175,6 +175,65 @@ k_gemm_4bit_256(int N, int M, int K, const T* __restrict__ A, const uint8_t* __r
   }
   __syncthreads();
 
+  if constexpr (M16 && XB) {
+    // Cross-barrier pipeline (as igemm_256.hip): tile t's k2 = 1 fragments are read into registers
+    // under its k2 = 0 MFMAs; after the barrier the wave reads tile t+1's k2 = 0 fragments under tile
+    // t's k2 = 1 MFMAs.  W(t+1) is dequantised into Ws[t+1] before the barrier as before.
+    // One set of A fragments is recycled row by row (a[i] is re-read right after its last MFMA), so
+    // only B is double-buffered: acc + 8 A + 2 x 4 B fragments fit the 256-VGPR budget.
+    uint4 a[8], b0[4], b1[4];
+    auto rd_a = [&](int buf, int k2, int i) {
+      return *reinterpret_cast<const uint4*>(smem + Q_OFF_X + buf * Q_XT + swz2(128 * wm + 16 * i + (lane & 15), 4 * k2 + (lane >> 4)));
+    };
+    auto rd_b = [&](int buf, int k2, uint4 (&b)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *reinterpret_cast<const uint4*>(smem + Q_OFF_W + buf * Q_WT + swz2(64 * wn + 16 * j + (lane & 15), 4 * k2 + (lane >> 4)));
+    };
+    rd_b(0, 0, b0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = rd_a(0, 0, i);
+    for (int t = 0; t < nk; ++t) {
+      const int s = t & 1;
+      uint8_t* wsn = smem + Q_OFF_W + (s ^ 1) * Q_WT;
+      uint32_t w4[4];
+      float am;
+      packed_of(s ^ 1, w4, am);                                    // W(t+1), landed during step t-1
+      rd_b(s, 1, b1);
+      if (t + 1 < nk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma_x_piece(t + 1, s ^ 1, i);  // every wave is past tile t-1's reads
+      }
+      if (t + 2 < nk) dma_w(t + 2, s);
+      float2 c0[4], c1[4];
+      lut_reads(w4[0], c0);
+      lut_reads(w4[1], c1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc16[i][j] = Mfma<T>::mma(a[i], b0[j], acc16[i][j]);
+        a[i] = rd_a(s, 1, i);
+      }
+      finish(c0, am, wsn, 0);
+      finish(c1, am, wsn, 1);
+      lut_reads(w4[2], c0);
+      lut_reads(w4[3], c1);
+      finish(c0, am, wsn, 2);
+      finish(c1, am, wsn, 3);
+      wait_vmcnt0();                                               // X(t+1), W(t+2) of this wave landed
+      __builtin_amdgcn_s_waitcnt(0xC07F);                          // its Ws[t+1] stores and tile-t reads done
+      __builtin_amdgcn_s_barrier();
+      const int sn = t + 1 < nk ? s ^ 1 : s;                       // (last step: harmless re-reads)
+      rd_b(sn, 0, b0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc16[i][j] = Mfma<T>::mma(a[i], b1[j], acc16[i][j]);
+        a[i] = rd_a(sn, 0, i);
+      }
+    }
+    __syncthreads();                                               // the epilogue reuses the stages
+  } else
   for (int t = 0; t < nk; ++t) {
     const int s = t & 1;
     const uint8_t* xs = smem + Q_OFF_X + s * Q_XT;
