@@ -252,6 +252,128 @@ k_igemm_xb(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __re
     *reinterpret_cast<uint4*>(out + (long long)grow * ldc + gcol) = make_uint4(lo.x, lo.y, hi.x, hi.y);
   }
 }
+
+// One wave per SIMD: 256 threads = 4 waves (2 x 2), 128 x 128 outputs per wave (8 x 8 tiles, 256
+// accumulator registers), so each fragment read from LDS feeds 8 MFMAs (4 in the 8-wave kernel).
+// Same stages, swizzle and cross-barrier fragment pipeline as the library kernel.
+__global__ void __launch_bounds__(256, 1)
+k_igemm_w4(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restrict__ B, fp16_t* __restrict__ out,
+           long long lda, long long ldb, long long ldc, const float* __restrict__ rowStats,
+           const float* __restrict__ colStats, const fp16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[J_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (N + 255) / 256, tilesM = (M + 255) / 256;
+  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  constexpr int GROUP = 4;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int8_t* asrc[8];
+  const int8_t* bsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = 8 * (8 * wave + i) + (lane >> 3);
+    const int ks = 16 * ((lane & 7) ^ (row & 7));
+    asrc[i] = A + (long long)min(m0 + row, M - 1) * lda + ks;
+    bsrc[i] = B + (long long)min(n0 + row, N - 1) * ldb + ks;
+  }
+  auto dma = [&](int kt, int buf) {
+    const long long k0 = (long long)kt * J_BK;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      glds16(asrc[i] + k0, smem + buf * J_TILE + (8 * wave + i) * 1024);
+      glds16(bsrc[i] + k0, smem + 2 * J_TILE + buf * J_TILE + (8 * wave + i) * 1024);
+    }
+  };
+  const int wm = wave >> 1, wn = wave & 1;
+  i32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = i32x4_t{0, 0, 0, 0};
+  uint4 fa[2][8], fb[2][8];
+  auto frag = [&](int buf, int ks, uint4 (&a)[8], uint4 (&b)[8]) {
+    const uint8_t* as = smem + buf * J_TILE;
+    const uint8_t* bs = smem + 2 * J_TILE + buf * J_TILE;
+    const int slot = 4 * ks + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz(128 * wn + 16 * j + (lane & 15), slot));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const uint4*>(as + swz(128 * wm + 16 * i + (lane & 15), slot));
+  };
+  auto mma = [&](const uint4 (&a)[8], const uint4 (&b)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a[i]), __builtin_bit_cast(i32x4_t, b[j]),
+                                                          acc[i][j], 0, 0, 0);
+  };
+  const int nk = K / J_BK;
+  dma(0, 0);
+  if (nk > 1) {
+    dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    wait_vmcnt0();
+  }
+  __syncthreads();
+  frag(0, 0, fa[0], fb[0]);
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    frag(s, 1, fa[1], fb[1]);
+    mma(fa[0], fb[0]);
+    wait_vmcnt0();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) dma(t + 2, s);
+    if (t + 1 < nk) frag(s ^ 1, 0, fa[0], fb[0]);
+    mma(fa[1], fb[1]);
+  }
+  __syncthreads();
+
+  // epilogue: fused mm_dequant, two 64-column halves through the per-wave [128][64] staging
+  const int grow0 = m0 + 128 * wm;
+  uint8_t* ep = smem + wave * (128 * J_EPI_STRIDE);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int gcol0 = n0 + 128 * wn + 64 * h;
+    float cs[4], bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = min(gcol0 + 16 * j + (lane & 15), N - 1);
+      cs[j] = colStats[col];
+      bv[j] = bias ? (float)bias[col] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * (lane >> 4) + r;
+        const float rs = rowStats[min(grow0 + row, M - 1)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<fp16_t*>(ep + row * J_EPI_STRIDE + 2 * (16 * j + (lane & 15))) =
+              mm_dequant_value(acc[i][4 * h + j][r], rs, cs[j], bv[j]);
+      }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int id = lane + 64 * it;
+      const int row = id >> 3, c8 = id & 7;
+      const int grow = grow0 + row, gcol = gcol0 + 8 * c8;
+      if (grow >= M || gcol + 8 > N) continue;
+      const uint2 lo = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8);
+      const uint2 hi = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8 + 8);
+      *reinterpret_cast<uint4*>(out + (long long)grow * ldc + gcol) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+}
 }  // namespace bnb
 using namespace bnb;
 
@@ -310,8 +432,8 @@ int main(int argc, char** argv) {
   vs.push_back({"lib 256 BK128 2-stage", lib, {}});
   vs.push_back({"3-stage BK64", v3(k_igemm_3s<0>), {}});
   vs.push_back({"cross-barrier", v3(k_igemm_xb<0>), {}});
-  vs.push_back({"xb sched_barrier", v3(k_igemm_xb<2>), {}});
-  vs.push_back({"xb sched_barrier x2", v3(k_igemm_xb<6>), {}});
+  auto w4 = [=]() { hipLaunchKernelGGL(k_igemm_w4, dim3(tiles), dim3(256), 0, 0, M, N, K, (const int8_t*)A, (const int8_t*)B, C1, (long long)K, (long long)K, (long long)N, (const float*)rs, (const float*)cs, (const fp16_t*)nullptr); };
+  vs.push_back({"one wave per SIMD", w4, {}});
   for (size_t v = 1; v < vs.size(); ++v) { vs[v].fn(); CK(hipDeviceSynchronize()); printf("%s", vs[v].name); check(); }
   for (int rep = 0; rep < 12; ++rep)
     for (auto& v : vs) {
