@@ -174,7 +174,7 @@ static int splitk_factor(int m, int n, int k) {
 
 long long gemm_4bit_workspace_bytes(int m, int n, int k) {
   const int ks = splitk_factor(m, n, k);
-  return ks > 1 ? (long long)ks * m * n * (long long)sizeof(float) : 0;
+  return std::max(ks > 1 ? (long long)ks * m * n * (long long)sizeof(float) : 0LL, skinny_workspace_bytes(m, n, k));
 }
 
 template <typename T>
@@ -185,6 +185,14 @@ void gemm_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* a
       ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) {
     set_error(1, "gemm_4bit: requires k % 64 == 0, lda % 8 == 0, ldb % 16 == 0, 16-B aligned A/B, blocksize >= 64");
     return;
+  }
+  // few tokens (<= 64): the weight-streaming kernel (gemm4bit_skinny.hip)
+  if (g_tile_override == 0) {
+    const SkStats st{absmax, nullptr, nullptr, nullptr, nullptr, 0, 0};
+    if (launch_gemm_4bit_skinny<T>(m, n, k, A, lda, B, ldb, st, blocksize, 0, datatype, out, ldc, ws, ws_bytes)) {
+      BNB_LAUNCH_CHECK("gemm_4bit");
+      return;
+    }
   }
   // m = out features (weight rows), n = tokens.  Large problems: 256x256 tiles (split-K when the
   // tile grid is too small and a workspace is given); small: 128x128.

@@ -82,4 +82,20 @@ template <typename T>
 void launch_gemm_4bit_256(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype,
                           T* out, int lda, int ldb, int ldc, int blocksize, float* ws, int ksplit);
 
+// Few-token kernel (gemm4bit_skinny.hip): 1..64 activation rows, K % 128 == 0.  Statistics either plain
+// fp32 absmax or nested (q8 + code2 + absmax2 + offset, decoded in-kernel).
+struct SkStats {
+  const float* absmax;
+  const uint8_t* q8;
+  const float* code2;
+  const float* absmax2;
+  const float* offset;
+  int bs_shift, bs2_shift;
+};
+long long skinny_workspace_bytes(int m, int n, int k);
+template <typename T>
+bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
+                             int blocksize, int blocksize2, const float* code, T* out, int ldc, float* ws,
+                             long long ws_bytes);
+
 }  // namespace bnb

@@ -42,11 +42,14 @@ class BNBNativeLibrary:
                      "cgemm_4bit_inference_naive_nested_fp16", "cgemm_4bit_inference_naive_nested_bf16",
                      "cdequantize_blockwise_nested_fp16_fp4", "cdequantize_blockwise_nested_fp16_nf4",
                      "cdequantize_blockwise_nested_bf16_fp4", "cdequantize_blockwise_nested_bf16_nf4",
-                     "cint8_row_quant_fp16"):
+                     "cint8_row_quant_fp16", "cgemm_4bit_inference_nested_ws_bf16",
+                     "cgemm_4bit_inference_nested_ws_fp16"):
             getattr(lib, name).restype = ct.c_int
 
     def __getattr__(self, item):
-        return getattr(self._lib, item)
+        fn = getattr(self._lib, item)
+        setattr(self, item, fn)          # later lookups hit the instance dict
+        return fn
 
 
 class _MissingLibrary:

@@ -8,6 +8,7 @@ there is no CPU/torch fallback for them.
 from __future__ import annotations
 
 import ctypes as ct
+import threading
 from functools import reduce
 import operator
 from typing import Any, Dict, Optional, Tuple
@@ -139,42 +140,73 @@ def get_special_format_str():
 
 # ----------------------------------------------------------------------------- call plumbing
 def is_on_gpu(tensors):
-    on_gpu = True
-    gpu_ids = set()
+    """All non-None tensors on one GPU (ref:functional.py:425-458), else TypeError."""
+    idx = None
     for t in tensors:
         if t is None:
             continue
-        on_gpu &= t.device.type == "cuda"
-        gpu_ids.add(t.device.index)
-    if not on_gpu:
-        raise TypeError(
-            "All input tensors need to be on the same GPU, but found some tensors to not be on a GPU:\n "
-            f"{[(t.shape, t.device) for t in tensors if t is not None]}",
-        )
-    if len(gpu_ids) > 1:
-        raise TypeError(
-            "Input tensors need to be on the same GPU, but found the following tensor and device combinations:\n "
-            f"{[(t.shape, t.device) for t in tensors if t is not None]}",
-        )
-    return on_gpu
+        if not t.is_cuda:
+            raise TypeError(
+                "All input tensors need to be on the same GPU, but found some tensors to not be on a GPU:\n "
+                f"{[(t.shape, t.device) for t in tensors if t is not None]}",
+            )
+        d = t.get_device()
+        if idx is None:
+            idx = d
+        elif d != idx:
+            raise TypeError(
+                "Input tensors need to be on the same GPU, but found the following tensor and device combinations:\n "
+                f"{[(t.shape, t.device) for t in tensors if t is not None]}",
+            )
+    return True
 
 
 def get_ptr(A: Optional[Tensor]) -> Optional[ct.c_void_p]:
     if A is None:
         return None
-    return ct.c_void_p(A.data.data_ptr())
+    return ct.c_void_p(A.data_ptr())
+
+
+# Host cost per call matters on the decode path (a 4096 x 11008 GEMV runs ~9 us on the GPU): the
+# device switch is skipped when the device is already current, and the library's (thread-local)
+# stream is rebound only when torch's current stream changed (cached per Python thread).
+_tls = threading.local()
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _current_raw_stream(idx: int) -> int:
+    if _raw_stream is not None:
+        return _raw_stream(idx)
+    return torch.cuda.current_stream(idx).cuda_stream
+
+
+def _offset_on(state, device) -> Tensor:
+    """The nested-statistics offset as a one-element fp32 tensor on `device` (only its pointer is passed)."""
+    off = state.offset
+    if torch.is_tensor(off) and off.is_cuda and off.dtype == torch.float32 and off.numel() == 1 and off.device == device:
+        return off
+    off = off if torch.is_tensor(off) else torch.tensor(float(off))
+    return off.to(device=device, dtype=torch.float32).reshape(1)
 
 
 def pre_call(device):
     """Select the device (ref:functional.py:461-464) and bind the library to torch's current stream."""
     prev_device = torch.cuda.current_device()
-    torch.cuda.set_device(device)
-    lib.cset_stream(ct.c_void_p(torch.cuda.current_stream(device).cuda_stream))
+    idx = device.index if isinstance(device, torch.device) else device
+    if idx is None:
+        idx = prev_device
+    if idx != prev_device:
+        torch.cuda.set_device(idx)
+    stream = _current_raw_stream(idx)
+    if getattr(_tls, "stream", None) != stream:
+        lib.cset_stream(ct.c_void_p(stream))
+        _tls.stream = stream
     return prev_device
 
 
 def post_call(prev_device):
-    torch.cuda.set_device(prev_device)
+    if torch.cuda.current_device() != prev_device:
+        torch.cuda.set_device(prev_device)
     err = lib.cget_last_error()
     if err:
         raise RuntimeError(f"bitsandbytes HIP kernel error: {lib.cget_last_error_message().decode()}")
@@ -454,8 +486,7 @@ def _dequant_4bit_nested(A: Tensor, state: QuantState, out: Tensor) -> bool:
     if out.dtype not in (torch.float16, torch.bfloat16) or state.absmax.dtype != torch.uint8:
         return False
     s2 = state.state2
-    offset = state.offset if torch.is_tensor(state.offset) else torch.tensor(float(state.offset))
-    offset = offset.to(device=A.device, dtype=torch.float32).reshape(1)
+    offset = _offset_on(state, A.device)
     prev_device = pre_call(A.device)
     is_on_gpu([A, state.absmax, s2.code, s2.absmax, offset, out])
     qt = "fp4" if state.quant_type == "fp4" else "nf4"
@@ -534,8 +565,7 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
         # compressed statistics decoded inside the GEMV kernel: one launch instead of
         # dequantize_blockwise + gemv (ref:functional.py:1982-1984)
         s2 = state.state2
-        offset = state.offset if torch.is_tensor(state.offset) else torch.tensor(float(state.offset))
-        offset = offset.to(device=A.device, dtype=torch.float32).reshape(1)
+        offset = _offset_on(state, A.device)
         is_on_gpu([B, A, out, state.absmax, s2.absmax, s2.code, offset, state.code])
         fn = getattr(lib, f"cgemm_4bit_inference_naive_nested_{names[A.dtype]}")
         rc = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A), get_ptr(B), get_ptr(state.absmax),
@@ -563,7 +593,8 @@ _GEMM_WS: dict = {}
 
 
 def _stream_key(device):
-    return torch.cuda.current_stream(device).cuda_stream
+    idx = device.index if isinstance(device, torch.device) else device
+    return _current_raw_stream(torch.cuda.current_device() if idx is None else idx)
 
 
 def _gemm_workspace(device, nbytes: int) -> Optional[Tensor]:
@@ -587,6 +618,9 @@ def _gemm_workspace(device, nbytes: int) -> Optional[Tensor]:
 # 4096 x 1024 108.7 vs 95.0; 1024 x 4096 108.2 vs 106.2; 512 x 4096 67.6 vs 80.4; 4096 x 512 69.6 vs 70.8.
 GEMM_4BIT_DEQUANT_MIN_ROWS = 2048
 GEMM_4BIT_DEQUANT_MIN_FEATURES = 1024
+# Up to this many activation rows the C side runs the weight-streaming kernel (gemm4bit_skinny.hip);
+# with nested statistics the Python side calls its one-launch entry point directly.
+GEMM_4BIT_FEW_TOKENS = 32
 
 _DEQ_WS: dict = {}
 _DEQ_META: dict = {}
@@ -624,11 +658,37 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         A2 = A2.contiguous()
     rows = A2.shape[0]
     library = rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES
-    if absmax is None and not (library and state.nested):
-        absmax = _absmax_fp32(state)
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
+    if (absmax is None and rows <= GEMM_4BIT_FEW_TOKENS and state.nested and state.absmax.dtype == torch.uint8
+            and state.absmax.is_contiguous()):
+        # few tokens, compressed statistics: one launch of the weight-streaming kernel that decodes the
+        # nested absmax in-kernel (no separate decode launch)
+        ws_bytes = int(lib.cgemm_4bit_workspace_bytes(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K)))
+        ws = _gemm_workspace(A.device, ws_bytes)
+        s2 = state.state2
+        offset = _offset_on(state, A.device)
+        prev_device = pre_call(A.device)
+        is_on_gpu([A2, Bc, out, state.absmax, s2.code, s2.absmax, offset, state.code])
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if events is not None else None
+        if ev:
+            ev[0].record()
+        fn = (lib.cgemm_4bit_inference_nested_ws_bf16 if A.dtype == torch.bfloat16
+              else lib.cgemm_4bit_inference_nested_ws_fp16)
+        rc = fn(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K), get_ptr(A2), get_ptr(Bc), get_ptr(state.absmax),
+                get_ptr(s2.code), get_ptr(s2.absmax), get_ptr(offset), get_ptr(state.code), get_ptr(out),
+                ct.c_int32(K), ct.c_int32((K + 1) // 2), ct.c_int32(N), ct.c_int32(state.blocksize),
+                ct.c_int32(s2.blocksize), get_ptr(ws), ct.c_longlong(ws_bytes))
+        if rc == 0:
+            post_call(prev_device)
+            if ev:
+                ev[1].record()
+                events.append(("gemm", ev[0], ev[1]))
+            return out.view(*A.shape[:-1], N)
+        post_call(prev_device)
+    if absmax is None and not (library and state.nested):
+        absmax = _absmax_fp32(state)
     prev_device = pre_call(A.device)
     is_on_gpu([A2, Bc, out, state.code] + ([absmax] if absmax is not None else []))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if events is not None else None

@@ -104,6 +104,20 @@ void cgemm_4bit_inference_code_ws_bf16(int m, int n, int k, bnb_bf16* A, unsigne
                                        float* datatype, bnb_bf16* out, int lda, int ldb, int ldc, int blocksize,
                                        float* workspace, long long workspace_bytes);
 long long cgemm_4bit_workspace_bytes(int m, int n, int k);
+/* [additive] few tokens (n <= 32, k % 128 == 0): the weight-streaming kernel with compressed statistics
+ * (absmax_q uint8 codes, code2 256-entry map, absmax2 per blocksize2 codes, offset: one fp32 on the
+ * device) decoded in-kernel -- replaces the absmax decode launch + GEMM of the M > 1 path
+ * (ref:functional.py:1346-1350 + autograd/_functions.py:507).  The plain-absmax calls above use the
+ * same kernel for n <= 32 when the workspace fits.  Returns 0 when launched, 1 when the shape,
+ * alignment or workspace does not fit (the caller then decodes absmax and uses the _ws entry points). */
+int cgemm_4bit_inference_nested_ws_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, unsigned char* absmax_q,
+                                        float* code2, float* absmax2, float* offset, float* datatype, bnb_fp16* out,
+                                        int lda, int ldb, int ldc, int blocksize, int blocksize2, float* workspace,
+                                        long long workspace_bytes);
+int cgemm_4bit_inference_nested_ws_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, unsigned char* absmax_q,
+                                        float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
+                                        int lda, int ldb, int ldc, int blocksize, int blocksize2, float* workspace,
+                                        long long workspace_bytes);
 /* [additive, testing] force the GEMM tile kernel: 0 = auto, 128 = 128x128, 256 = 256x256 */
 void cgemm_4bit_set_tile(int tile);
 

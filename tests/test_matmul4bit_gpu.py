@@ -185,12 +185,20 @@ def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
     caller workspace, summed in split order, one cast.  Same tolerance as the unsplit kernel."""
     F = _F()
     M, N, K = mnk
-    assert F.lib.cgemm_4bit_workspace_bytes(N, M, K) == ks * M * N * 4
+    # (few-token shapes run the weight-streaming kernel by default: force the 256x256 kernel here)
+    few = M <= F.GEMM_4BIT_FEW_TOKENS
+    assert F.lib.cgemm_4bit_workspace_bytes(N, M, K) >= ks * M * N * 4
+    if not few:
+        assert F.lib.cgemm_4bit_workspace_bytes(N, M, K) == ks * M * N * 4
     torch.manual_seed(M + 7 * N)
     W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
     X = torch.randn(M, K, device=dev, dtype=dtype)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
-    Y = F.gemm_4bit(X, q, st)
+    F.lib.cgemm_4bit_set_tile(256 if few else 0)
+    try:
+        Y = F.gemm_4bit(X, q, st)
+    finally:
+        F.lib.cgemm_4bit_set_tile(0)
     exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), st.absmax.cpu().numpy(), N, K, 64,
                                     st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
@@ -199,9 +207,13 @@ def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
     # without a workspace the dispatcher falls back to an unsplit kernel: same result up to fp32 order
     out = torch.empty_like(Y)
     fn = F.lib.cgemm_4bit_inference_code_bf16 if dtype == torch.bfloat16 else F.lib.cgemm_4bit_inference_code_fp16
-    fn(ct.c_int32(N), ct.c_int32(M), ct.c_int32(K), F.get_ptr(X), F.get_ptr(q), F.get_ptr(st.absmax),
-       F.get_ptr(st.code), F.get_ptr(out), ct.c_int32(K), ct.c_int32(K // 2), ct.c_int32(N), ct.c_int32(64))
-    torch.cuda.synchronize()
+    F.lib.cgemm_4bit_set_tile(256 if few else 0)
+    try:
+        fn(ct.c_int32(N), ct.c_int32(M), ct.c_int32(K), F.get_ptr(X), F.get_ptr(q), F.get_ptr(st.absmax),
+           F.get_ptr(st.code), F.get_ptr(out), ct.c_int32(K), ct.c_int32(K // 2), ct.c_int32(N), ct.c_int32(64))
+        torch.cuda.synchronize()
+    finally:
+        F.lib.cgemm_4bit_set_tile(0)
     rms = Y.float().pow(2).mean().sqrt().item()
     assert (Y.float() - out.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Y.float().abs().max().item()
 
@@ -325,3 +337,74 @@ def test_gemm_4bit_library_path_two_streams(dev):
         torch.cuda.synchronize()
         for i in range(2):
             assert torch.equal(outs[i], ref_out[i])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("mnk", [(2, 11008, 4096), (3, 300, 1152), (16, 4096, 11008), (17, 1000, 2048),
+                                 (33, 64, 128), (48, 520, 640), (64, 4096, 4096), (64, 11008, 4096)])
+def test_gemm_4bit_few_tokens_vs_oracle(dev, dtype, nested, mnk):
+    """1..64 activation rows (batched decode, short prefill) run the weight-streaming kernel
+    (gemm4bit_skinny.hip): same dequantised weights, fp32 sums split over K in split order.  Nested
+    statistics are decoded in the kernel.  Same tolerance as the tile kernels; ragged rows, one-block K,
+    a tail chunk (K = 11008 = 86 blocks) and single-split shapes."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M * 7 + N)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    Y = F.gemm_4bit(X, q, st)
+    assert Y.shape == (M, N) and Y.dtype == dtype
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64,
+                                    st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
+    assert frac == 0.0, err
+    # the tile kernels (forced) agree up to fp32 summation order
+    F.lib.cgemm_4bit_set_tile(128)
+    try:
+        Yt = F.gemm_4bit(X, q, st, absmax=F._absmax_fp32(st))
+    finally:
+        F.lib.cgemm_4bit_set_tile(0)
+    rms = Yt.float().pow(2).mean().sqrt().item()
+    assert (Y.float() - Yt.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Yt.float().abs().max().item()
+
+
+def test_gemm_4bit_few_tokens_nested_matches_plain(dev):
+    """In-kernel decode of compressed statistics = the decoded fp32 absmax passed in: bit-identical."""
+    F = _F()
+    M, N, K = 24, 4096, 11008
+    torch.manual_seed(5)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    Yn = F.gemm_4bit(X, q, st)
+    Yp = F.gemm_4bit(X, q, st, absmax=F._absmax_fp32(st))
+    assert torch.equal(Yn, Yp)
+    # deterministic: the split partials are summed in a fixed order
+    assert torch.equal(Yn, F.gemm_4bit(X, q, st))
+
+
+def test_gemm_4bit_few_tokens_entry_point_declines(dev):
+    """The one-launch entry point returns 1 (nothing launched) when the shape does not fit it."""
+    F = _F()
+    M, N, K = 65, 256, 1024                     # > 64 tokens
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16), blocksize=64,
+                            quant_type="nf4", compress_statistics=True)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    s2 = st.state2
+    off = st.offset.reshape(1).float()
+    rc = F.lib.cgemm_4bit_inference_nested_ws_bf16(
+        ct.c_int32(N), ct.c_int32(M), ct.c_int32(K), F.get_ptr(X), F.get_ptr(q), F.get_ptr(st.absmax),
+        F.get_ptr(s2.code), F.get_ptr(s2.absmax), F.get_ptr(off), F.get_ptr(st.code), F.get_ptr(out),
+        ct.c_int32(K), ct.c_int32(K // 2), ct.c_int32(N), ct.c_int32(64), ct.c_int32(s2.blocksize), None,
+        ct.c_longlong(0))
+    assert rc == 1
+    Y = F.gemm_4bit(X, q, st)                  # routed to the tile kernels
+    Wd = F.dequantize_4bit(q, st)
+    Yref = X.float() @ Wd.float().t()
+    rms = Yref.pow(2).mean().sqrt().item()
+    assert (Y.float() - Yref).abs().max().item() < 2e-2 * rms + 2e-2 * Yref.abs().max().item()
