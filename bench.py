@@ -128,6 +128,32 @@ def bench_decode_gemv(dev, iters=30):
     return res
 
 
+def bench_few_token_gemm(dev, iters=30, tokens=(2, 8, 16, 32)):
+    """Batched decode / short prefill on the config-2 weight (11008 x 4096 NF4, nested statistics, the
+    Linear4bit default): gemm_4bit with 2..32 activation rows runs the weight-streaming kernel
+    (gemm4bit_skinny.hip, + its ordered split-K reduce).  14 rotating weight copies, HIP-graph replay;
+    GB/s over the algorithmic bytes (packed weights + nested stats + activations + output)."""
+    n_out, k_in, copies = 11008, 4096, 14
+    g = torch.Generator(device=dev).manual_seed(3)
+    ws = []
+    for _ in range(copies):
+        W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        ws.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True))
+        del W
+    res = {"shape": [None, n_out, k_in], "path": "k_gemm_4bit_skinny (+ k_skinny_reduce)"}
+    for m in tokens:
+        x = torch.randn(m, k_in, device=dev, dtype=torch.bfloat16, generator=g)
+        out = torch.empty(m, n_out, device=dev, dtype=torch.bfloat16)
+        calls = [(lambda q=q, st=st: F.gemm_4bit(x, q, st, out=out)) for q, st in ws]
+        t = _time_graph(calls, iters)
+        nbytes = (n_out * k_in // 2 + n_out * k_in // BS + n_out * k_in // BS // 256 * 4 + 1024 + 4
+                  + m * k_in * 2 + m * n_out * 2)
+        res[f"tokens_{m}"] = {"us": t * 1e6, "gbs": nbytes / t / 1e9, "frac_of_hbm": nbytes / t / 1e9 / PEAK_HBM_GBS,
+                              "tflops": 2.0 * m * n_out * k_in / t / 1e12}
+    res["note"] = "14 rotating weight copies (~355 MB) defeat the 256 MB MALL; HIP-graph replay (kernel time)"
+    return res
+
+
 def bench_dequant_config1(dev, iters=30):
     """Config 1 on the GPU: dequantize_blockwise NF4 of a 4096x4096 weight, bs=64 -> bf16 (HBM-bound)."""
     g = torch.Generator(device=dev).manual_seed(0)
@@ -420,6 +446,7 @@ def main():
         extras["int8_igemmlt_metric_shape"] = bench_int8(dev, M, N, K)
         extras["int8_igemmlt_config3"] = bench_int8(dev, 4096, 4096, 4096)
         extras["decode_gemv_config2"] = bench_decode_gemv(dev)
+        extras["few_token_gemm_config2_weight"] = bench_few_token_gemm(dev)
         extras["dequant_nf4_config1_gpu"] = bench_dequant_config1(dev)
         extras["optimizer_adam8bit_blockwise"] = bench_optimizer_8bit(dev)
         extras["nf4_fused_kernel_metric_shape"] = bench_nf4_fused_kernel(dev)
