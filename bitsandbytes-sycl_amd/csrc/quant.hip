@@ -521,51 +521,20 @@ BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_fp16_nf4, fp16_t, NF4)
 BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_bf16_fp4, bf16_t, FP4)
 BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_bf16_nf4, bf16_t, NF4)
 
-// Host-pointer entry points (ref:sycl/pythonInterface.cpp:419-420).  Executed on the current
-// GPU: stage -> kernel -> copy back (synchronous, like the reference CPU path).
-void cquantize_blockwise_cpu_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize,
-                                  long long n) {
-  if (n <= 0 || blocksize <= 0) return;
-  const long long nb = (n + blocksize - 1) / blocksize;
-  float *d_code = nullptr, *d_A = nullptr, *d_absmax = nullptr;
-  uint8_t* d_out = nullptr;
-  hipStream_t s = current_stream();
-  if (hipMalloc(&d_code, 256 * sizeof(float)) != hipSuccess || hipMalloc(&d_A, n * sizeof(float)) != hipSuccess ||
-      hipMalloc(&d_absmax, nb * sizeof(float)) != hipSuccess || hipMalloc(&d_out, n) != hipSuccess) {
-    set_error(2, "cquantize_blockwise_cpu_fp32: hipMalloc failed");
-  } else {
-    code[0] = -1.0f;   // documented in-place side effect of the reference (cpu_ops.cpp:20)
-    hipMemcpyAsync(d_code, code, 256 * sizeof(float), hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(d_A, A, n * sizeof(float), hipMemcpyHostToDevice, s);
-    hipLaunchKernelGGL(k_quantize_cpu_semantics, dim3((unsigned)nb), dim3(256), 0, s, d_code, d_A, d_absmax, d_out, blocksize, n);
-    BNB_LAUNCH_CHECK("quantize_cpu_semantics");
-    hipMemcpyAsync(absmax, d_absmax, nb * sizeof(float), hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-  }
-  hipFree(d_code); hipFree(d_A); hipFree(d_absmax); hipFree(d_out);
-}
+// The host-pointer entry points cquantize_blockwise_cpu_fp32 / cdequantize_blockwise_cpu_fp32
+// (ref:sycl/pythonInterface.cpp:419-420) run on the host cores: cpu_ops.cpp.
 
-void cdequantize_blockwise_cpu_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize,
+// [additive] device-pointer form of the CPU-path quantize (the same division / nearest-code semantics,
+// one byte per element, any blocksize) executed on the GPU; `code` is a device pointer and is NOT
+// rewritten (the kernel uses code[0] = -1 internally).
+void cquantize_blockwise_bytes_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize,
                                     long long n) {
   if (n <= 0 || blocksize <= 0) return;
   const long long nb = (n + blocksize - 1) / blocksize;
-  float *d_code = nullptr, *d_absmax = nullptr, *d_out = nullptr;
-  uint8_t* d_A = nullptr;
-  hipStream_t s = current_stream();
-  if (hipMalloc(&d_code, 256 * sizeof(float)) != hipSuccess || hipMalloc(&d_A, n) != hipSuccess ||
-      hipMalloc(&d_absmax, nb * sizeof(float)) != hipSuccess || hipMalloc(&d_out, n * sizeof(float)) != hipSuccess) {
-    set_error(2, "cdequantize_blockwise_cpu_fp32: hipMalloc failed");
-  } else {
-    hipMemcpyAsync(d_code, code, 256 * sizeof(float), hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(d_A, A, n, hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(d_absmax, absmax, nb * sizeof(float), hipMemcpyHostToDevice, s);
-    hipLaunchKernelGGL(k_dequantize_cpu_semantics, dim3(stream_grid(n, 256)), dim3(256), 0, s, d_code, d_A, d_absmax, d_out, blocksize, n);
-    BNB_LAUNCH_CHECK("dequantize_cpu_semantics");
-    hipMemcpyAsync(out, d_out, n * sizeof(float), hipMemcpyDeviceToHost, s);
-    hipStreamSynchronize(s);
-  }
-  hipFree(d_code); hipFree(d_A); hipFree(d_absmax); hipFree(d_out);
+  if (nb > 0x7fffffffLL) { set_error(1, "quantize_bytes: too many blocks"); return; }
+  hipLaunchKernelGGL(k_quantize_cpu_semantics, dim3((unsigned)nb), dim3(256), 0, current_stream(), code, A, absmax,
+                     out, blocksize, n);
+  BNB_LAUNCH_CHECK("quantize_bytes");
 }
 
 // [additive] nested statistics -> fp32 absmax in one launch (replaces dequantize_blockwise + the

@@ -341,9 +341,12 @@ def quantize_blockwise(A: Tensor, code: Optional[Tensor] = None, absmax: Optiona
         fn(get_ptr(code), get_ptr(A), get_ptr(absmax), get_ptr(out), ct.c_int32(blocksize), ct.c_int(A.numel()))
         post_call(prev_device)
     else:
-        # host tensors: the reference's CPU entry point (executed by the library on the GPU)
+        # host tensors: the reference's CPU entry point (ref:functional.py:885-895), run on the host cores by
+        # the library (cpu_ops.cpp; no GPU needed).  It takes fp32 only: other dtypes are converted first
+        # (the reference passes their pointer unchanged and the C side misreads them).
         code = code.cpu()
-        lib.cquantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(A), get_ptr(absmax), get_ptr(out),
+        A32 = A if (A.dtype == torch.float32 and A.is_contiguous()) else A.float().contiguous()
+        lib.cquantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(A32), get_ptr(absmax), get_ptr(out),
                                          ct.c_longlong(blocksize), ct.c_longlong(A.numel()))
 
     if nested:
@@ -393,9 +396,15 @@ def dequantize_blockwise(A: Tensor, quant_state: Optional[QuantState] = None, ab
            ct.c_int(A.numel()))
         post_call(prev_device)
     else:
+        # host tensors (ref:functional.py:1006-1015), run on the host cores.  The decoded fp32 absmax is passed
+        # (the reference passes quant_state.absmax, i.e. the uint8 codes, when the statistics are nested).
         code = quant_state.code.cpu()
-        lib.cdequantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(A), get_ptr(quant_state.absmax), get_ptr(out),
+        absmax = absmax.float().contiguous()
+        o32 = out if (out.dtype == torch.float32 and out.is_contiguous()) else torch.empty(A.shape, dtype=torch.float32)
+        lib.cdequantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(A.contiguous()), get_ptr(absmax), get_ptr(o32),
                                            ct.c_longlong(quant_state.blocksize), ct.c_longlong(A.numel()))
+        if o32 is not out:
+            out.copy_(o32)
     return out
 
 

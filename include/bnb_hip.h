@@ -55,11 +55,16 @@ void cdequantize_blockwise_bf16_fp4(float* code, unsigned char* A, float* absmax
 void cdequantize_blockwise_bf16_nf4(float* code, unsigned char* A, float* absmax, bnb_bf16* out, int blocksize, const int n); /* :221 */
 
 /* ---- host-pointer CPU-path entry points: ref:sycl/pythonInterface.cpp:419-420 (cpu_ops.cpp semantics:
- * division A/absmax, nearest code with ties to the left, code[0] := -1 in place).  Executed on the GPU
- * (host buffers staged through HBM), synchronous on return. */
+ * division A/absmax, nearest code with ties to the left, code[0] := -1 in place).  Run on the host cores
+ * (csrc/cpu_ops.cpp; no HIP call, so they work without a GPU), synchronous on return. */
 void cquantize_blockwise_cpu_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize, long long n);   /* :419 */
 void cdequantize_blockwise_cpu_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize, long long n); /* :420 */
-/* [additive] device-pointer form of the CPU-path dequantize (one byte per element, any blocksize) */
+/* [additive] worker threads of the two host entry points (0 = default: BNB_CPU_THREADS or the hardware
+ * threads, at most 64); returns the count in effect */
+int cset_cpu_threads(int threads);
+/* [additive] device-pointer forms of the CPU-path quantize / dequantize, executed on the GPU (one byte per
+ * element, any blocksize; the quantize does not rewrite the caller's code table) */
+void cquantize_blockwise_bytes_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize, long long n);
 void cdequantize_blockwise_bytes_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize, long long n);
 
 /* ---- 4-bit GEMV (M == 1): ref:sycl/pythonInterface.cpp:408-415 ----

@@ -166,24 +166,29 @@ def test_nested_absmax_one_launch_ragged(dev, n):
     assert same_bits(out.cpu().numpy(), ref.nested_absmax(q, a2, code.numpy(), off))
 
 
-def test_cpu_path_entry_points(golden, dev):
-    """cquantize_blockwise_cpu_fp32 / cdequantize_blockwise_cpu_fp32 (host pointers, cpu_ops.cpp semantics)."""
+def test_cpu_semantics_on_device(golden, dev):
+    """[additive] cquantize_blockwise_bytes_fp32 / cdequantize_blockwise_bytes_fp32: the CPU path's semantics
+    (division, nearest code, code[0] = -1) on device pointers, bit-exact against the CPU-path fixtures; the
+    caller's device code table is not rewritten.  (The host entry points themselves: tests/test_cpu_path.py.)"""
     F = _F()
-    A = torch.from_numpy(golden["cpu_A"].copy())
-    code = torch.from_numpy(create_dynamic_map().copy())
-    absmax = torch.zeros((A.numel() + 63) // 64)
-    out = torch.zeros(A.numel(), dtype=torch.uint8)
-    F.lib.cquantize_blockwise_cpu_fp32(F.get_ptr(code), F.get_ptr(A), F.get_ptr(absmax), F.get_ptr(out),
-                                       ct.c_longlong(64), ct.c_longlong(A.numel()))
-    assert F.lib.cget_last_error() == 0
-    assert code[0].item() == -1.0                              # in-place side effect (cpu_ops.cpp:20)
-    assert same_bits(absmax.numpy(), golden["cpu_absmax"])
-    assert same_bits(out.numpy(), golden["cpu_q"])
-    y = torch.zeros(A.numel())
-    F.lib.cdequantize_blockwise_cpu_fp32(F.get_ptr(code), F.get_ptr(out), F.get_ptr(absmax), F.get_ptr(y),
+    A = torch.from_numpy(golden["cpu_A"].copy()).to(dev)
+    code = torch.from_numpy(create_dynamic_map().copy()).to(dev)
+    absmax = torch.zeros((A.numel() + 63) // 64, device=dev)
+    out = torch.zeros(A.numel(), dtype=torch.uint8, device=dev)
+    F.lib.cquantize_blockwise_bytes_fp32(F.get_ptr(code), F.get_ptr(A), F.get_ptr(absmax), F.get_ptr(out),
                                          ct.c_longlong(64), ct.c_longlong(A.numel()))
-    assert same_bits(y.numpy(), golden["cpu_deq"])
-    # the functional CPU route goes through the same entry points
+    torch.cuda.synchronize()
+    assert F.lib.cget_last_error() == 0
+    assert code[0].item() != -1.0
+    assert same_bits(absmax.cpu().numpy(), golden["cpu_absmax"])
+    assert same_bits(out.cpu().numpy(), golden["cpu_q"])
+    code_after = torch.from_numpy(golden["cpu_code_after"]).to(dev)
+    y = torch.zeros(A.numel(), device=dev)
+    F.lib.cdequantize_blockwise_bytes_fp32(F.get_ptr(code_after), F.get_ptr(out), F.get_ptr(absmax), F.get_ptr(y),
+                                           ct.c_longlong(64), ct.c_longlong(A.numel()))
+    torch.cuda.synchronize()
+    assert same_bits(y.cpu().numpy(), golden["cpu_deq"])
+    # the functional CPU route (host cores) gives the same codes as the device form
     q2, st = F.quantize_blockwise(torch.from_numpy(golden["cpu_A"].copy()), blocksize=64)
     assert same_bits(q2.numpy(), golden["cpu_q"])
 
