@@ -32,7 +32,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import python_src_quants.functional as F  # noqa: E402
-from python_src_quants.parallel import sharded_forward_overlapped  # noqa: E402
+from python_src_quants.parallel import (ColumnShardedLinear8bitLt, shard_quantized_4bit,  # noqa: E402
+                                        sharded_forward_overlapped)
 
 M, N, K = 4096, 4096, 11008
 BS = 64
@@ -83,6 +84,61 @@ def bench_int8(dev, m, n, k, iters=20):
     return {"shape": [m, n, k], "tops": ops / t_gemm / 1e12, "us": t_gemm * 1e6,
             "frac_of_int8_peak": ops / t_gemm / 1e12 / PEAK_INT8_TOPS,
             "forward_with_double_quant_us": t_fwd * 1e6, "forward_inference_row_quant_us": t_inf * 1e6}
+
+
+def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
+    """The metric's INT8 half at 1/2/4/8 GPUs: Linear8bitLt's CB/SCB [n, k] sharded by output
+    feature (ColumnShardedLinear8bitLt, rows of CB), the fp16 activations replicated and row-quantised on every
+    rank (int8_row_quant, no exchange), the fused igemmlt + dequant on the rank's rows, one RCCL all-gather of the
+    fp16 output (token-row chunks overlap the gather with the next chunk's GEMM).  Same barrier + max-over-ranks
+    timing as the main step; TOPS = 2*m*n*k / step time (whole job)."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    A = (torch.randn(m, k, device=dev, generator=g) * 2).half()
+    Wt = (torch.randn(n, k, device=dev, generator=g) * 0.05).half()
+    CB, _, SCB, _, _ = F.double_quant(Wt)
+    del Wt
+    lin = ColumnShardedLinear8bitLt(CB, SCB, world, rank)
+    del CB
+    ev = []
+
+    def step(record=False):
+        if record:
+            s0, e0 = _events()
+            s0.record()
+        if world > 1:
+            lin.forward(A, assemble=False, chunks=chunks)
+        else:
+            lin.forward_local(A)
+        if record:
+            e0.record()
+            ev.append((s0, e0))
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    per = elapsed / steps
+    ops = 2.0 * m * n * k
+    import statistics
+    med = statistics.median(s.elapsed_time(e) for s, e in ev) * 1e-3
+    return {"shape": [m, n, k], "n_gpus": world, "tops": ops / per / 1e12, "ms_per_step": per * 1e3,
+            "median_step_ms_rank0": med * 1e3,
+            "step": "int8_row_quant(X) + fused igemmlt+dequant on this rank's CB rows" +
+                    (f" + RCCL all_gather ({chunks} chunks)" if world > 1 else ""),
+            "frac_of_int8_peak": ops / per / 1e12 / PEAK_INT8_TOPS}
 
 
 def _time_graph(calls, iters):
@@ -271,12 +327,35 @@ def bench_llama2_7b_prefill(dev, batch=32, seq=2048, iters=3):
     return res
 
 
+def host_cpu_info():
+    """The GPU box's host CPU as the bench sees it: model name (/proc/cpuinfo), logical CPUs of the machine and
+    the CPUs this process may run on (the box gives a job a share of a larger machine)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"model": model, "nproc_machine": os.cpu_count(), "cpus_usable": usable,
+            "torch_threads": torch.get_num_threads()}
+
+
 def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
     """Reference CPU path as ported (oracle/cpu_ops_port.cpp, the restated cpu_ops.cpp dequantize_cpu,
     single-threaded as written) + torch CPU F.linear (the CPU path has no GEMM), on a
     bounded sample: per repetition the full W [4096, 11008] is dequantised and multiplied with `rows`
-    activation rows; repetitions run until ~budget_s of CPU work, the median rep is reported."""
+    activation rows; repetitions run until ~budget_s of CPU work, the median rep is reported.  Beside it,
+    config 1 itself (NF4 4096 x 4096, bs 64, one index byte per element) through the port and through the
+    product's host entry point cdequantize_blockwise_cpu_fp32 (csrc/cpu_ops.cpp, multi-threaded)."""
     import numpy as np
+    import statistics
     sys.path.insert(0, ROOT)
     from oracle.maps import nf4_padded_256
     lib = ct.CDLL(os.path.join(ROOT, "oracle", "_build", "libcpu_ops_port.so"))
@@ -290,27 +369,48 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
     X = torch.randn(rows, K)
     threads = torch.get_num_threads()
     torch.nn.functional.linear(X[:8], Wt)
+    vp = lambda a: a.ctypes.data_as(ct.c_void_p)   # noqa: E731
     deq, mm = [], []
     start = time.perf_counter()
     while len(deq) < max_reps and (time.perf_counter() - start) < budget_s:
         t0 = time.perf_counter()
-        lib.port_dequantize_cpu(code.ctypes.data_as(ct.c_void_p), idx.ctypes.data_as(ct.c_void_p),
-                                absmax.ctypes.data_as(ct.c_void_p), W.ctypes.data_as(ct.c_void_p),
-                                ct.c_longlong(BS), ct.c_longlong(n_el))
+        lib.port_dequantize_cpu(vp(code), vp(idx), vp(absmax), vp(W), ct.c_longlong(BS), ct.c_longlong(n_el))
         t1 = time.perf_counter()
         torch.nn.functional.linear(X, Wt)
         t2 = time.perf_counter()
         deq.append(t1 - t0)
         mm.append(t2 - t1)
-    import statistics
     t_deq, t_mm = statistics.median(deq), statistics.median(mm)
     flops = 2.0 * rows * N * K
     value = flops / (t_deq + t_mm) / 1e12
+
+    # config 1 (4096 x 4096 NF4, bs 64): 16 MiB of index bytes + 1 MiB absmax -> 64 MiB fp32
+    n1 = 4096 * 4096
+    i1, a1, o1 = idx[:n1], absmax[:n1 // BS], W[:n1]
+    c1_bytes = n1 + n1 // BS * 4 + n1 * 4
+    t_port, t_prod = [], []
+    prod_threads = int(F.lib.cset_cpu_threads(0))
+    for _ in range(5):
+        t0 = time.perf_counter()
+        lib.port_dequantize_cpu(vp(code), vp(i1), vp(a1), vp(o1), ct.c_longlong(BS), ct.c_longlong(n1))
+        t1 = time.perf_counter()
+        F.lib.cdequantize_blockwise_cpu_fp32(vp(code), vp(i1), vp(a1), vp(o1), ct.c_longlong(BS), ct.c_longlong(n1))
+        t2 = time.perf_counter()
+        t_port.append(t1 - t0)
+        t_prod.append(t2 - t1)
+    tp, tq = statistics.median(t_port), statistics.median(t_prod)
     return {"value": value, "unit": "TFLOP/s", "cores": threads, "kind": "port",
             "sample": f"{len(deq)} reps of: dequantize_cpu (1 thread, as ref:sycl/cpu_ops.cpp:7-14) of W[{N},{K}] "
                       f"NF4 bs=64 unpacked ({t_deq:.3f}s, {n_el * 9 / t_deq / 1e9:.2f} GB/s) + torch CPU fp32 "
-                      f"F.linear on {rows} of the {M} rows ({t_mm:.3f}s, {threads} threads); median rep",
-            "dequant_cpu_gbs": n_el * 9 / t_deq / 1e9}
+                      f"F.linear on {rows} of the {M} rows ({t_mm:.3f}s, {threads} torch threads); median rep",
+            "cores_per_leg": {"dequantize_cpu": 1, "torch_linear": threads},
+            "host": host_cpu_info(),
+            "dequant_cpu_gbs": n_el * 9 / t_deq / 1e9,
+            "config1_cpu": {"shape": [4096, 4096], "bytes": c1_bytes,
+                            "port_1_thread": {"ms": tp * 1e3, "gbs": c1_bytes / tp / 1e9},
+                            "product_cpu_path": {"ms": tq * 1e3, "gbs": c1_bytes / tq / 1e9, "threads": prod_threads,
+                                                 "entry": "cdequantize_blockwise_cpu_fp32 (csrc/cpu_ops.cpp)"},
+                            "note": "median of 5; same inputs; outputs bit-identical (tests/test_cpu_path.py)"}}
 
 
 def gemm_kernel_name(m, n, k=K):
@@ -345,6 +445,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-extras", action="store_true", help="skip int8/decode/config-1/cpu legs")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-int8", action="store_true", help="skip the sharded int8 leg")
     ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 ranks on one GPU")
@@ -368,10 +469,16 @@ def main():
     # ---- synthetic data (same global problem for every world size)
     gx = torch.Generator(device=dev).manual_seed(1)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=gx)
-    gw = torch.Generator(device=dev).manual_seed(1000 + rank)
-    W = (torch.randn(shard, K, device=dev, generator=gw) * 0.02).to(torch.bfloat16)
-    q, st = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True)
+    # the full weight, quantised once (nested statistics, the Linear4bit default) and sliced per rank by the
+    # product's shard_quantized_4bit -- what a rank does with a pre-quantised checkpoint (no float weight)
+    gw = torch.Generator(device=dev).manual_seed(1000)
+    W = (torch.randn(N, K, device=dev, generator=gw) * 0.02).to(torch.bfloat16)
+    q_full, st_full = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True)
     del W
+    q, st = shard_quantized_4bit(q_full, st_full, world, rank)
+    if world > 1:
+        q = q.clone()
+        del q_full
     Y = torch.empty(M, shard, device=dev, dtype=torch.bfloat16)
     chunks = args.chunks if (world > 1 and args.chunks >= 1 and M % args.chunks == 0) else 1
     Mc = M // chunks
@@ -380,9 +487,14 @@ def main():
 
     library = gemm_kernel_name(Mc, shard).startswith("hipBLASLt")
 
+    step_ev = []
+
     def step(record=False):
         # fused kernel: nested stats -> fp32 absmax once per step, shared by the chunks; library path:
         # gemm_4bit decodes them inside its dequantise launch
+        if record:
+            s0, e0 = _events()
+            s0.record()
         absmax = None if library else F._absmax_fp32(st)
         ev = []
 
@@ -400,6 +512,8 @@ def main():
             mm(X, Y)
         if record:
             kev.append(ev)
+            e0.record()
+            step_ev.append((s0, e0))
 
     # clock ramp: MI355X takes ~0.1-0.3 s of sustained MFMA load to reach its steady clock; run the
     # step untimed for --prewarm-ms before the W counted warmup steps (the timed region is unchanged)
@@ -441,7 +555,12 @@ def main():
     shard_flops = 2.0 * Mc * shard * K
     achieved = shard_flops / kern_s / 1e12
 
+    import statistics
+    median_step_ms = statistics.median(s.elapsed_time(e) for s, e in step_ev)
+
     extras = {}
+    if not args.no_int8:     # every rank: it contains collectives when world > 1
+        extras["int8_igemmlt_sharded"] = bench_int8_sharded(dev, world, rank, args.steps, args.warmup, chunks)
     if rank == 0 and world == 1 and not args.no_extras:
         extras["int8_igemmlt_metric_shape"] = bench_int8(dev, M, N, K)
         extras["int8_igemmlt_config3"] = bench_int8(dev, 4096, 4096, 4096)
@@ -473,6 +592,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "median_step_ms_rank0": round(median_step_ms, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

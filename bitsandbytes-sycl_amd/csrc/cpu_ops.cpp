@@ -11,8 +11,8 @@
 //   dequantize out[i] = code[A[i]] * absmax[i / blocksize] (cpu_ops.cpp:7-14), one byte per element.
 // Execution differs (results do not): instead of one OS thread per block in waves of 256
 // (cpu_ops.cpp:31-61; 262,144 thread creations at config 1) and a single-threaded dequantize, blocks are
-// split into contiguous ranges over a bounded number of worker threads (BNB_CPU_THREADS or
-// cset_cpu_threads; default: the hardware threads, at most 64).  Every element's value depends only on
+// split into contiguous ranges over a bounded number of worker threads (cset_cpu_threads, else BNB_CPU_THREADS,
+// else OMP_NUM_THREADS, else the hardware threads, at most 64).  Every element's value depends only on
 // its own block, so the split cannot change a result.
 #include <algorithm>
 #include <atomic>
@@ -30,9 +30,11 @@ std::atomic<int> g_cpu_threads{0};
 int cpu_threads() {
   int t = g_cpu_threads.load();
   if (t > 0) return t;
-  if (const char* e = std::getenv("BNB_CPU_THREADS")) {
-    t = std::atoi(e);
-    if (t > 0) return t;
+  for (const char* var : {"BNB_CPU_THREADS", "OMP_NUM_THREADS"}) {   // the job's CPU share, when the host says
+    if (const char* e = std::getenv(var)) {
+      t = std::atoi(e);
+      if (t > 0) return t;
+    }
   }
   t = (int)std::thread::hardware_concurrency();
   if (t <= 0) t = 1;

@@ -229,8 +229,8 @@ k_skinny_reduce(const float* __restrict__ ws, int nsplit, int M, int N, T* __res
   }
 }
 
-// Blocks of 128 k per workgroup: the activation slice (NB x 16 MT rows x 256 B) stays within ~40 KiB of LDS
-// so three workgroups fit a CU; all of a workgroup's weights are in flight at once (NB x 16 B per lane).
+// Blocks of 128 k per workgroup: the activation slice ((NB + 1) x 16 MT rows x 256 B = 44 / 48 KiB at MT 1 / 2,
+// plus the pair table and code2: 47 / 51 KiB in all) lets three workgroups fit a CU; all of a workgroup's weights are in flight at once (NB x 16 B per lane).
 template <int MT> constexpr int skinny_nb() { return MT == 1 ? 10 : 5; }
 
 static int skinny_tiles(int n) { return (n + 15) / 16; }

@@ -87,7 +87,7 @@ class MatMul8bitLt(torch.autograd.Function):
             state.idx = idx
         # 2. quantise B (once, unless training fp16 weights)
         if state.has_fp16_weights:
-            has_grad = getattr(B, "grad", None) is not None
+            has_grad = B.is_leaf and B.grad is not None
             is_transposed = not B.is_contiguous() and B.shape[0] == B.stride(1)
             if is_transposed:
                 B = B.contiguous()
@@ -190,7 +190,11 @@ class MatMul4Bit(torch.autograd.Function):
             if A.shape[-1] == B_shape[0]:
                 return torch.empty(A.shape[:-1] + B_shape[1:], dtype=A.dtype, device=A.device)
             return torch.empty(A.shape[:-1] + B_shape[:1], dtype=A.dtype, device=A.device)
-        if F.gemm_4bit_supported(A, quant_state):
+        # B as the reference passes it: the transposed view of the packed weight (Linear4bit's weight.t(),
+        # shape (1, n/2)) means out = A @ W^T with W [shape[0], shape[1]] -- the fused GEMM's orientation; the
+        # untransposed storage (shape (n/2, 1)) means out = A @ W (dequantize_4bit's is_transposed rule,
+        # ref:functional.py:1420-1424), which takes the dequantise + matmul path
+        if B.shape[0] == 1 and F.gemm_4bit_supported(A, quant_state):
             output = F.gemm_4bit(A, B, quant_state)
             if bias is not None:
                 output = output + bias
@@ -228,7 +232,7 @@ def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: F.QuantState, out
                 bias=None):
     """Routing of ref:autograd/_functions.py:557-577: one activation row without grad -> gemv_4bit."""
     assert quant_state is not None
-    if A.numel() == A.shape[-1] and A.requires_grad is False:
+    if A.numel() == A.shape[-1] and A.requires_grad is False and B.shape[0] == 1:
         if A.shape[-1] % quant_state.blocksize != 0:
             warnings.warn(
                 f"Some matrices hidden dimension is not a multiple of {quant_state.blocksize} and efficient inference "

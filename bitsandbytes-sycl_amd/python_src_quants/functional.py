@@ -465,6 +465,18 @@ def dequantize_nf4(A, quant_state=None, absmax=None, out=None, blocksize: int = 
     return dequantize_4bit(A, quant_state, absmax, out, blocksize, "nf4")
 
 
+def _nested_stats_in_kernel_ok(state: QuantState) -> bool:
+    """Compressed statistics a kernel can decode in place: contiguous uint8 codes, a contiguous fp32 second level
+    and a contiguous fp32 256-entry map, a power-of-two nested blocksize (what the in-kernel decoders read)."""
+    if not state.nested or state.absmax.dtype != torch.uint8 or not state.absmax.is_contiguous():
+        return False
+    s2 = state.state2
+    bs2 = s2.blocksize
+    return (s2.absmax.dtype == torch.float32 and s2.absmax.is_contiguous() and s2.code is not None
+            and s2.code.dtype == torch.float32 and s2.code.is_contiguous() and s2.code.numel() >= 256
+            and bs2 > 0 and (bs2 & (bs2 - 1)) == 0)
+
+
 def _absmax_fp32(state: QuantState) -> Tensor:
     """Per-block fp32 absmax, resolving nested statistics (ref:functional.py:1346-1350, 1982-1984)."""
     absmax = state.absmax
@@ -492,7 +504,7 @@ def _absmax_fp32(state: QuantState) -> Tensor:
 def _dequant_4bit_nested(A: Tensor, state: QuantState, out: Tensor) -> bool:
     """One launch: the 4-bit dequantise with the compressed statistics decoded in the kernel
     (cdequantize_blockwise_nested_*).  False when the dtype/shape needs the two-step path."""
-    if out.dtype not in (torch.float16, torch.bfloat16) or state.absmax.dtype != torch.uint8:
+    if out.dtype not in (torch.float16, torch.bfloat16) or not _nested_stats_in_kernel_ok(state):
         return False
     s2 = state.state2
     offset = _offset_on(state, A.device)
@@ -570,7 +582,7 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
     names = {torch.float16: "fp16", torch.bfloat16: "bf16", torch.float32: "fp32"}
     if A.dtype not in names:
         raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
-    if state.nested and A.dtype != torch.float32 and state.absmax.dtype == torch.uint8:
+    if A.dtype != torch.float32 and _nested_stats_in_kernel_ok(state):
         # compressed statistics decoded inside the GEMV kernel: one launch instead of
         # dequantize_blockwise + gemv (ref:functional.py:1982-1984)
         s2 = state.state2
@@ -670,8 +682,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
-    if (absmax is None and rows <= GEMM_4BIT_FEW_TOKENS and state.nested and state.absmax.dtype == torch.uint8
-            and state.absmax.is_contiguous()):
+    if (absmax is None and not library and rows <= GEMM_4BIT_FEW_TOKENS and _nested_stats_in_kernel_ok(state)):
         # few tokens, compressed statistics: one launch of the weight-streaming kernel that decodes the
         # nested absmax in-kernel (no separate decode launch)
         ws_bytes = int(lib.cgemm_4bit_workspace_bytes(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K)))

@@ -38,6 +38,53 @@ def shard_packed_rows(packed: torch.Tensor, absmax: torch.Tensor, shape, blocksi
     return p, a
 
 
+def shard_quantized_4bit(packed: torch.Tensor, state: "F.QuantState", world: int, rank: int):
+    """Rank `rank`'s output-feature shard of an already quantised 4-bit weight [N, K] (e.g. a Linear4bit or an
+    NF4 checkpoint restored by Params4bit.from_prequantized, ref:nn/modules.py:271-289), without the float weight.
+
+    Returns (packed_shard [(n*K)//2, 1] uint8, QuantState with shape (n, K)).  The packed bytes and the first-level
+    block statistics are sliced (K % blocksize == 0: no block straddles two rows).  Compressed (nested) statistics,
+    the Linear4bit default (ref:nn/modules.py:385; layout ref:functional.py:1243-1257), are handled two ways:
+      * the shard starts on a second-level block (its first block index is a multiple of the nested blocksize,
+        true for every Llama-2-70B projection at 8 ranks): the uint8 codes and their fp32 second-level scales are
+        sliced too, with the full weight's offset -- the shard decodes to exactly the full weight's block scales;
+      * otherwise the shard's fp32 block scales are decoded and re-compressed for the shard alone (offset = their
+        mean, dynamic 8-bit map, the nested blocksize) -- what quantize_4bit would store for these rows."""
+    N, K = state.shape
+    bs = state.blocksize
+    if K % bs or K % 2:
+        raise ValueError("row sharding needs K % blocksize == 0 and even K")
+    start, end = shard_range(N, world, rank)
+    n = end - start
+    b0, b1 = start * K // bs, end * K // bs
+    flat = packed.reshape(-1)
+    p = flat[start * K // 2:end * K // 2].reshape(-1, 1)
+    shape = torch.Size([n, K])
+    if not state.nested:
+        return p, F.QuantState(absmax=state.absmax[b0:b1], shape=shape, code=state.code, blocksize=bs,
+                               quant_type=state.quant_type, dtype=state.dtype)
+    s2 = state.state2
+    bs2 = s2.blocksize
+    if b0 % bs2 == 0:
+        e2 = (b1 + bs2 - 1) // bs2
+        state2 = F.QuantState(absmax=s2.absmax[b0 // bs2:e2], blocksize=bs2, code=s2.code, dtype=s2.dtype)
+        return p, F.QuantState(absmax=state.absmax[b0:b1], shape=shape, code=state.code, blocksize=bs,
+                               quant_type=state.quant_type, dtype=state.dtype, offset=state.offset, state2=state2)
+    absmax = F._absmax_fp32(state)[b0:b1].contiguous()
+    offset = absmax.mean()
+    qabsmax, state2 = F.quantize_blockwise(absmax - offset, blocksize=bs2)
+    return p, F.QuantState(absmax=qabsmax, shape=shape, code=state.code, blocksize=bs, quant_type=state.quant_type,
+                           dtype=state.dtype, offset=offset, state2=state2)
+
+
+def shard_int8_rows(CB: torch.Tensor, SCB: torch.Tensor, world: int, rank: int):
+    """Rank `rank`'s output-feature shard of an LLM.int8 weight: the rows of CB (int8 [N, K], row-normalised) and
+    of its row statistics SCB (fp32 [N]) -- Int8Params' state (ref:nn/modules.py:559-632).  Rows quantise
+    independently, so the slice is exactly what double_quant gives for those rows."""
+    start, end = shard_range(CB.shape[0], world, rank)
+    return CB[start:end], SCB[start:end]
+
+
 def gather_columns(y_local: torch.Tensor, world: int, group=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """All-gather the per-rank [M, n] slices into [world, M, n] (one collective; RCCL on GPU)."""
     if world == 1:
@@ -100,17 +147,36 @@ def gathered_to_rows(g: torch.Tensor) -> torch.Tensor:
 class ColumnShardedLinear4bit(torch.nn.Module):
     """Holds this rank's NF4/FP4 shard of a linear layer's weight and runs the sharded forward."""
 
-    def __init__(self, weight: torch.Tensor, world: int, rank: int, group=None, quant_type: str = "nf4",
+    def __init__(self, weight: Optional[torch.Tensor], world: int, rank: int, group=None, quant_type: str = "nf4",
                  blocksize: int = 64, compress_statistics: bool = True, device=None):
         super().__init__()
-        n_out, k_in = weight.shape
         self.world, self.rank, self.group = world, rank, group
+        if weight is None:      # filled by from_quantized
+            return
+        n_out, k_in = weight.shape
         self.start, self.end = shard_range(n_out, world, rank)
         device = device or torch.device("cuda", torch.cuda.current_device())
         w = weight[self.start:self.end].to(device)
         self.qweight, self.quant_state = F.quantize_4bit(w, blocksize=blocksize, quant_type=quant_type,
                                                          compress_statistics=compress_statistics)
         self.out_features, self.in_features = n_out, k_in
+
+    @classmethod
+    def from_quantized(cls, packed: torch.Tensor, state: "F.QuantState", world: int, rank: int, group=None,
+                       device=None) -> "ColumnShardedLinear4bit":
+        """This rank's shard of an already quantised weight (a Linear4bit's packed bytes + QuantState, or a
+        pre-quantised checkpoint), sliced by shard_quantized_4bit -- no float weight is needed on any rank."""
+        self = cls(None, world, rank, group)
+        n_out, k_in = state.shape
+        self.start, self.end = shard_range(n_out, world, rank)
+        p, st = shard_quantized_4bit(packed, state, world, rank)
+        if device is not None:
+            p = p.to(device)
+            st.to(device)
+            st.code = st.code.to(device)
+        self.qweight, self.quant_state = p, st
+        self.out_features, self.in_features = n_out, k_in
+        return self
 
     def forward_local(self, x: torch.Tensor) -> torch.Tensor:
         x2 = x.reshape(-1, self.in_features)
@@ -133,4 +199,45 @@ class ColumnShardedLinear4bit(torch.nn.Module):
             g = sharded_forward_overlapped(x2, mm, self.world, self.group, chunks)
             return chunked_to_rows(g) if assemble else g
         g = gather_columns(self.forward_local(x), self.world, self.group)
+        return gathered_to_rows(g) if assemble else g
+
+
+class ColumnShardedLinear8bitLt(torch.nn.Module):
+    """LLM.int8 counterpart: this rank holds rows [start, end) of CB/SCB; every rank quantises the
+    replicated activations itself (int8_row_quant: no exchange), runs the fused igemmlt + dequant on its rows, and
+    one RCCL all-gather assembles the fp16 output columns."""
+
+    def __init__(self, CB: torch.Tensor, SCB: torch.Tensor, world: int, rank: int, group=None,
+                 bias: Optional[torch.Tensor] = None):
+        super().__init__()
+        self.world, self.rank, self.group = world, rank, group
+        self.out_features, self.in_features = CB.shape
+        self.start, self.end = shard_range(self.out_features, world, rank)
+        self.CB, self.SCB = shard_int8_rows(CB, SCB, world, rank)
+        self.CB = self.CB.contiguous()
+        self.bias = None if bias is None else bias[self.start:self.end].contiguous()
+
+    @classmethod
+    def from_linear(cls, layer, world: int, rank: int, group=None) -> "ColumnShardedLinear8bitLt":
+        """Shard a quantised nn.Linear8bitLt (after .cuda(): CB/SCB on the weight, or in its state after a
+        forward)."""
+        CB = layer.weight.CB if layer.weight.CB is not None else layer.state.CB
+        SCB = layer.weight.SCB if layer.weight.SCB is not None else layer.state.SCB
+        bias = None if layer.bias is None else layer.bias.data.half()
+        return cls(CB, SCB, world, rank, group, bias)
+
+    def forward_local(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        x2 = x.reshape(-1, self.in_features)
+        if x2.dtype != torch.float16:
+            x2 = x2.half()
+        CA, SCA = F.int8_row_quant(x2)
+        return F.igemmlt_dequant(CA, self.CB, SCA, self.SCB, bias=self.bias, out=out)
+
+    def forward(self, x: torch.Tensor, assemble: bool = True, chunks: int = 1) -> torch.Tensor:
+        x2 = x.reshape(-1, self.in_features)
+        if chunks > 1:
+            g = sharded_forward_overlapped(x2, lambda xc, yc: self.forward_local(xc, yc), self.world, self.group,
+                                           chunks)
+            return chunked_to_rows(g) if assemble else g
+        g = gather_columns(self.forward_local(x2), self.world, self.group)
         return gathered_to_rows(g) if assemble else g

@@ -59,8 +59,8 @@ void cdequantize_blockwise_bf16_nf4(float* code, unsigned char* A, float* absmax
  * (csrc/cpu_ops.cpp; no HIP call, so they work without a GPU), synchronous on return. */
 void cquantize_blockwise_cpu_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize, long long n);   /* :419 */
 void cdequantize_blockwise_cpu_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize, long long n); /* :420 */
-/* [additive] worker threads of the two host entry points (0 = default: BNB_CPU_THREADS or the hardware
- * threads, at most 64); returns the count in effect */
+/* [additive] worker threads of the two host entry points (0 = default: BNB_CPU_THREADS, else OMP_NUM_THREADS,
+ * else the hardware threads, at most 64); returns the count in effect */
 int cset_cpu_threads(int threads);
 /* [additive] device-pointer forms of the CPU-path quantize / dequantize, executed on the GPU (one byte per
  * element, any blocksize; the quantize does not rewrite the caller's code table) */

@@ -1,0 +1,95 @@
+"""The BASELINE.json configurations at their full sizes, on the routes the product takes for them.
+
+* Metric shape (M=4096, N=4096, K=11008, NF4 bs=64, nested statistics): functional.gemm_4bit as routed (and the
+  fused kernel forced), against the fp64 oracle ref.gemm_4bit_dequant_ref (the reference's M > 1 algorithm,
+  ref:autograd/_functions.py:491-507) on 256 sampled rows x all columns.
+* Config 4: the three distinct Llama-2-7B projection shapes (4096x4096, 11008x4096, 4096x11008) at 2048 tokens.
+* Config 5: one 8-way column shard of each Llama-2-70B projection (q/o 8192x8192, k/v 1024x8192,
+  gate/up 28672x8192, down 8192x28672, each N/8) at 2048 tokens, from a full-size quantised weight sliced by
+  parallel.shard_quantized_4bit (packed bytes, uint8 codes and second-level scales sliced: every 70B shard starts
+  on a second-level block) -- its statistics decode to the full weight's exactly.
+* Config 2 (decode) is covered in test_matmul4bit_gpu.py; config 3 and the int8 metric shape in
+  test_int8_gpu.py (exact int32 against a float64 GPU product, then mm_dequant bit-exact).
+Tolerance: BASELINE.md §5 -- |d| <= 2e-2 * rms + 2e-2 * |ref| for bf16 outputs, mean |d| < 0.115."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _F():
+    import python_src_quants.functional as F
+    return F
+
+
+def _check_rows(Y, X, q, absmax, N, K, code, rows):
+    exp = ref.gemm_4bit_dequant_ref(X[rows].float().cpu().numpy(), q.cpu().numpy(), absmax.cpu().numpy(), N, K, 64,
+                                    code.cpu().numpy(), "bf16")
+    got = Y[rows].float().cpu().numpy().astype(np.float64)
+    rms = np.sqrt(np.mean(exp ** 2))
+    err = np.abs(got - exp)
+    assert np.all(err <= 2e-2 * rms + 2e-2 * np.abs(exp)), float(err.max())
+    assert err.mean() < 0.115
+
+
+def _sample_rows(M, dev, n=256, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randperm(M, generator=g)[:n].sort().values.to(dev)
+
+
+def _quantized(N, K, dev, seed):
+    F = _F()
+    g = torch.Generator(device=dev).manual_seed(seed)
+    W = (torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    del W
+    return q, st
+
+
+@pytest.mark.parametrize("route", ["routed", "fused"])
+def test_metric_shape(dev, route, monkeypatch):
+    F = _F()
+    M, N, K = 4096, 4096, 11008
+    q, st = _quantized(N, K, dev, 1000)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=torch.Generator(device=dev).manual_seed(1))
+    if route == "fused":
+        monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1 << 30)
+    Y = F.gemm_4bit(X, q, st)
+    _check_rows(Y, X, q, F._absmax_fp32(st), N, K, st.code, _sample_rows(M, dev))
+
+
+@pytest.mark.parametrize("n_out,k_in", [(4096, 4096), (11008, 4096), (4096, 11008)])
+def test_llama2_7b_projections(dev, n_out, k_in):
+    F = _F()
+    M = 2048
+    q, st = _quantized(n_out, k_in, dev, n_out + k_in)
+    X = torch.randn(M, k_in, device=dev, dtype=torch.bfloat16)
+    Y = F.gemm_4bit(X, q, st)
+    assert Y.shape == (M, n_out)
+    _check_rows(Y, X, q, F._absmax_fp32(st), n_out, k_in, st.code, _sample_rows(M, dev, seed=n_out))
+
+
+@pytest.mark.parametrize("name,n_out,k_in", [("q_o", 8192, 8192), ("k_v", 1024, 8192), ("gate_up", 28672, 8192),
+                                             ("down", 8192, 28672)])
+def test_llama2_70b_shard(dev, name, n_out, k_in):
+    """Rank 3 of 8: its N/8 rows of the quantised full weight, via the product's shard function."""
+    F = _F()
+    from python_src_quants.parallel import shard_quantized_4bit
+    world, rank, M = 8, 3, 2048
+    q, st = _quantized(n_out, k_in, dev, n_out // 7 + k_in)
+    qs, sts = shard_quantized_4bit(q, st, world, rank)
+    n = n_out // world
+    assert sts.shape == (n, k_in) and sts.nested
+    X = torch.randn(M, k_in, device=dev, dtype=torch.bfloat16)
+    Y = F.gemm_4bit(X, qs, sts)
+    assert Y.shape == (M, n)
+    # every 70B shard starts on a second-level block: its statistics decode to the full weight's exactly
+    full = F._absmax_fp32(st)[rank * n * k_in // 64:(rank + 1) * n * k_in // 64]
+    part = F._absmax_fp32(sts)
+    assert torch.equal(part, full)
+    _check_rows(Y, X, qs, part, n, k_in, sts.code, _sample_rows(M, dev, seed=n))
+    # and the shard's packed bytes are the full weight's rows [rank*n, (rank+1)*n)
+    assert torch.equal(qs.reshape(-1), q.reshape(-1)[rank * n * k_in // 2:(rank + 1) * n * k_in // 2])

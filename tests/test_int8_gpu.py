@@ -162,8 +162,13 @@ def test_igemmlt_row_dequant_fused(dev, mnk):
                             bias=torch.from_numpy(bias).to(dev))
     C = F.igemm_rowmajor(At, Bt)
     if m * n * k <= 2e8:
-        assert np.array_equal(C.cpu().numpy(), ref.igemmlt(A, B))
-    exp = ref.mm_dequant(C.cpu().numpy(), rs, cs, bias)
+        exact = ref.igemmlt(A, B)
+    else:
+        # at the benched sizes: an exact float64 product on the GPU (|sum| <= 127^2 * k < 2^53), an independent
+        # check of the int32 result the fused epilogue consumes
+        exact = (At.double() @ Bt.double().T).cpu().numpy().astype(np.int64).astype(np.int32)
+    assert np.array_equal(C.cpu().numpy(), exact)
+    exp = ref.mm_dequant(exact, rs, cs, bias)
     assert same_bits(out.cpu().numpy(), exp)
 
 

@@ -344,7 +344,7 @@ def test_gemm_4bit_library_path_two_streams(dev):
 @pytest.mark.parametrize("mnk", [(2, 11008, 4096), (3, 300, 1152), (16, 4096, 11008), (17, 1000, 2048),
                                  (33, 64, 128), (48, 520, 640), (64, 4096, 4096), (64, 11008, 4096)])
 def test_gemm_4bit_few_tokens_vs_oracle(dev, dtype, nested, mnk):
-    """1..64 activation rows (batched decode, short prefill) run the weight-streaming kernel
+    """1..32 activation rows (batched decode, short prefill) run the weight-streaming kernel; 33..64 the tile kernels
     (gemm4bit_skinny.hip): same dequantised weights, fp32 sums split over K in split order.  Nested
     statistics are decoded in the kernel.  Same tolerance as the tile kernels; ragged rows, one-block K,
     a tail chunk (K = 11008 = 86 blocks) and single-split shapes."""
@@ -390,7 +390,7 @@ def test_gemm_4bit_few_tokens_nested_matches_plain(dev):
 def test_gemm_4bit_few_tokens_entry_point_declines(dev):
     """The one-launch entry point returns 1 (nothing launched) when the shape does not fit it."""
     F = _F()
-    M, N, K = 65, 256, 1024                     # > 64 tokens
+    M, N, K = 33, 256, 1024                     # > 32 tokens (SK_MAX_TOKENS)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     q, st = F.quantize_4bit((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16), blocksize=64,
                             quant_type="nf4", compress_statistics=True)
@@ -408,3 +408,37 @@ def test_gemm_4bit_few_tokens_entry_point_declines(dev):
     Yref = X.float() @ Wd.float().t()
     rms = Yref.pow(2).mean().sqrt().item()
     assert (Y.float() - Yref).abs().max().item() < 2e-2 * rms + 2e-2 * Yref.abs().max().item()
+
+
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("qt,bs", [("nf4", 64), ("fp4", 64), ("nf4", 128), ("fp4", 256)])
+@pytest.mark.parametrize("mnk", [(5, 1001, 2048), (24, 4099, 4096), (3, 63, 128), (32, 1, 256)])
+def test_gemm_4bit_few_tokens_ragged_n(dev, nested, qt, bs, mnk):
+    """Few-token kernel on out_features not a multiple of 4 (the scalar partial-store and reduce tails), split-K
+    shapes, FP4 and blocksizes 128 / 256, nested and plain statistics -- against the fp64 oracle."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M + N + bs)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
+    Y = F.gemm_4bit(X, q, st)
+    assert Y.shape == (M, N)
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, bs,
+                                    st.code.cpu().numpy(), "bf16")
+    frac, err = _close(Y.float().cpu().numpy(), exp, 2e-2, 2e-2)
+    assert frac == 0.0, err
+
+
+def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
+    """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 forces the dequantise + library GEMM route for few tokens too (the few-token
+    branch is not taken): the result equals dequantize_4bit + torch.matmul bit for bit."""
+    F = _F()
+    monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1)
+    M, N, K = 8, 2048, 1024
+    torch.manual_seed(31)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    assert torch.equal(F.gemm_4bit(X, q, st), torch.matmul(X, F.dequantize_4bit(q, st).t()))

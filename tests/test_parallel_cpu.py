@@ -114,3 +114,105 @@ def test_overlapped_chunked_allgather_gloo():
     ret = mgr.dict()
     mp.spawn(_worker_overlap, args=(world, port, ret), nprocs=world, join=True)
     assert all(ret[r] for r in range(world))
+
+
+def _worker_nested(rank, world, port, ret):
+    """Each rank shards a NESTED quantised weight with the product's shard_quantized_4bit (no float weight), on CPU
+    tensors: sliced second level when the shard starts on a 256-block boundary, re-compressed otherwise."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "bitsandbytes-sycl_amd")]
+    from oracle import ref
+    import python_src_quants.functional as F
+    from python_src_quants.parallel import gather_columns, gathered_to_rows, shard_quantized_4bit
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ok = True
+        bs = 64
+        # (N, K): 512 x 64 -> 256 rows per rank = 256 blocks (aligned); 24 x 128 -> 12 rows = 24 blocks (not)
+        for N, K, aligned in ((512, 64, True), (24, 128, False)):
+            M = 3
+            rng = np.random.default_rng(N)
+            W = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+            X = rng.standard_normal((M, K)).astype(np.float32)
+            absmax, q = ref.quantize_blockwise(W.reshape(-1), bs, "nf4")
+            am = torch.from_numpy(absmax)
+            offset = am.mean()
+            qam, st2 = F.quantize_blockwise(am - offset, blocksize=256)       # the product's CPU path
+            state = F.QuantState(absmax=qam, shape=torch.Size([N, K]), code=torch.from_numpy(ref.nf4_table()),
+                                 blocksize=bs, quant_type="nf4", dtype=torch.float32, offset=offset, state2=st2)
+            decoded = F._absmax_fp32(state).numpy()
+            p, sst = shard_quantized_4bit(torch.from_numpy(q).reshape(-1, 1), state, world, rank)
+            n = N // world
+            ok &= tuple(sst.shape) == (n, K) and sst.nested
+            ok &= bool(np.array_equal(p.numpy().reshape(-1), q[rank * n * K // 2:(rank + 1) * n * K // 2]))
+            part = F._absmax_fp32(sst).numpy()
+            full = decoded[rank * n * K // bs:(rank + 1) * n * K // bs]
+            if aligned:
+                ok &= bool(np.array_equal(part, full))
+            else:
+                ok &= bool(np.abs(part - full).max() <= 0.02 * np.abs(full).max())
+            y_local = ref.gemm_4bit_dequant_ref(X, p.numpy(), part, n, K, bs, ref.nf4_table(), "fp32")
+            g = gather_columns(torch.from_numpy(y_local.astype(np.float32)), world)
+            got = gathered_to_rows(g).numpy()
+            if aligned:
+                exp = ref.gemm_4bit_dequant_ref(X, q, decoded, N, K, bs, ref.nf4_table(), "fp32").astype(np.float32)
+                ok &= bool(np.array_equal(got, exp))
+            else:
+                exp = ref.gemm_4bit_dequant_ref(X, q, absmax, N, K, bs, ref.nf4_table(), "fp32")
+                ok &= bool(np.abs(got - exp).max() <= 0.05 * np.abs(exp).max())
+        ret[rank] = ok
+    finally:
+        dist.destroy_process_group()
+
+
+def test_nested_shard_from_quantized_gloo():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_nested, args=(world, port, ret), nprocs=world, join=True)
+    assert all(ret[r] for r in range(world))
+
+
+def _worker_int8(rank, world, port, ret):
+    """LLM.int8 output-feature shard: CB/SCB rows via the product's shard_int8_rows; activations quantised on every
+    rank (replicated); the gathered fp16 output equals the unsharded igemmlt + mm_dequant bit for bit."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "bitsandbytes-sycl_amd")]
+    from oracle import ref
+    from python_src_quants.parallel import gather_columns, gathered_to_rows, shard_int8_rows, shard_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(7)
+        M, N, K = 9, 64, 96
+        A = (rng.standard_normal((M, K)) * 2).astype(np.float16)
+        Wt = (rng.standard_normal((N, K)) * 0.1).astype(np.float16)
+        rsW, csW, _ = ref.colrow_absmax(Wt)
+        CB, _ = ref.double_quant(Wt, rsW, csW)
+        rsA, csA, _ = ref.colrow_absmax(A)
+        CA, _ = ref.double_quant(A, rsA, csA)
+        cb, scb = shard_int8_rows(torch.from_numpy(CB), torch.from_numpy(rsW), world, rank)
+        s, e = shard_range(N, world, rank)
+        y_local = ref.mm_dequant(ref.igemmlt(CA, cb.numpy()), rsA, scb.numpy())
+        g = gather_columns(torch.from_numpy(y_local), world)
+        exp = ref.mm_dequant(ref.igemmlt(CA, CB), rsA, rsW)
+        ret[rank] = bool(np.array_equal(gathered_to_rows(g).numpy(), exp)) and cb.shape == (e - s, K)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_int8_row_shard_gloo():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_int8, args=(world, port, ret), nprocs=world, join=True)
+    assert all(ret[r] for r in range(world))
