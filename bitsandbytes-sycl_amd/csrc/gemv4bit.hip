@@ -281,6 +281,148 @@ k_gemv_4bit_dot(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
   }
 }
 
+// One workgroup per CU (the decode weights of one layer fit in flight at once, <= 16 x 16 B per lane).
+// k_gemv_4bit_dot gives every workgroup 4 waves x R rows, so at 11008 rows the 688 workgroups land 2, 3 or 4
+// per CU and the kernel ends with the most loaded CU; here workgroup g of G = min(256, M) owns the balanced
+// row range [g*M/G, (g+1)*M/G) (43 rows at 11008), so every CU streams the same bytes.
+// Wave w takes rows r0 + w + 8j (j < RMAX), clamped to the range: a clamped row re-reads the range's last row,
+// which the owning wave of the same CU is loading at the same moment (an L2 hit, no extra HBM bytes), and its
+// sum is dropped.  Each lane takes chunks lane + 64u (u < U), clamped the same way.  All RMAX x U weight loads
+// are issued before any is consumed, in consumption order (u outer, rows inner), so the compiler's counted
+// waits retire them one by one.  Same table / dot / statistics arithmetic as k_gemv_4bit_dot (bit-identical).
+constexpr int GC_THREADS = 512, GC_WAVES = GC_THREADS / 64;
+
+template <typename T, int U, int RMAX, bool NESTED>
+__global__ void __launch_bounds__(GC_THREADS, 1)
+k_gemv_4bit_cu(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
+               const float* __restrict__ datatype, T* __restrict__ out, int ldb, int G) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
+  uint8_t* table = gsm;                               // GV_TABLE_BYTES
+  uint8_t* xs = gsm + GV_TABLE_BYTES;                 // K * 2 bytes
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r0 = (int)((long long)blockIdx.x * M / G), r1 = (int)((long long)(blockIdx.x + 1) * M / G);
+  const int nch = K >> 5;
+  const long long two_ldb = 2LL * ldb;
+  auto row_of = [&](int j) { return min(r0 + wave + GC_WAVES * j, r1 - 1); };
+  auto chunk_of = [&](int u) { return min(lane + 64 * u, nch - 1); };
+
+  // (1a) block statistics; the 16 code values by scalar loads
+  float dt[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dt[j] = datatype[j];
+  float am[U][RMAX];
+  uint32_t q8[U][RMAX];
+  float a2[U][RMAX];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      const long long blk = (two_ldb * row_of(j) + 32LL * chunk_of(u)) >> st.bs_shift;
+      if constexpr (NESTED) {
+        q8[u][j] = st.q8[blk];
+        a2[u][j] = st.absmax2[blk >> st.bs2_shift];
+      } else {
+        am[u][j] = st.absmax[blk];
+      }
+    }
+  float offset = 0.0f, c2 = 0.0f;
+  if constexpr (NESTED) {
+    offset = *st.offset;
+    c2 = st.code2[threadIdx.x & 255];
+  }
+  // (1b) activations by LDS-DMA (1 KiB per wave-instruction)
+  const int nx = K >> 3;
+  for (int p = wave; p * 64 < nx; p += GC_WAVES) {
+    const int idx = p * 64 + lane;
+    if (idx < nx) glds16(A + 8 * idx, xs + p * 1024);
+  }
+  // (1c) every weight chunk of this wave, non-temporal, behind the DMA (laundered pointer)
+  uintptr_t bp = (uintptr_t)B;
+  asm volatile("" : "+s"(bp)::"memory");
+  uint4 b[U][RMAX];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      const u32x4_t v =
+          __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row_of(j) * ldb + 16LL * chunk_of(u)));
+      b[u][j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  // (2) 32 bank-private copies of the pair table: entry e of copy c at byte 128 e + 4 c (512 threads x 4 stores)
+  static_assert(GC_THREADS == 512, "table fill assumes 512 threads");
+  {
+    const int e_lo = (threadIdx.x >> 3) & 15;         // e & 15 for every store of this thread
+    float lo = dt[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) lo = e_lo == j ? dt[j] : lo;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = threadIdx.x + k * GC_THREADS;     // 16-B store index: entry i >> 3, copies 4 (i & 7) ..
+      const int e_hi = (i >> 3) >> 4;                 // = 4 k + (tid >> 7)
+      float hi = dt[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) hi = e_hi == j ? dt[j] : hi;
+      const uint32_t v = Dot2<T>::pair(hi, lo);
+      *reinterpret_cast<uint4*>(table + (i >> 3) * 128 + 16 * (i & 7)) = make_uint4(v, v, v, v);
+    }
+  }
+  float* code2s = reinterpret_cast<float*>(xs + 2 * K);
+  if constexpr (NESTED) {
+    if (threadIdx.x < 256) code2s[threadIdx.x] = c2;
+  }
+  // (3) activations landed (only this wave's RMAX * U weight loads may be outstanding), table visible
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U * RMAX) : "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  if constexpr (NESTED) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) am[u][j] = __fadd_rn(__fmul_rn(code2s[q8[u][j]], a2[u][j]), offset);
+  }
+  float acc[RMAX];
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) acc[j] = 0.0f;
+  const uint32_t lane4 = (lane & 31) * 4;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool valid = lane + 64 * u < nch;
+    const int c = chunk_of(u);
+    uint32_t x[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(xs + 64 * c)[q];
+      x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      const uint32_t w[4] = {b[u][j].x, b[u][j].y, b[u][j].z, b[u][j].w};
+      uint32_t l[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        l[i] = *reinterpret_cast<const uint32_t*>(table + ((((w[i >> 2] >> (8 * (i & 3))) & 0xFF) << 7) | lane4));
+      float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        s0 = Dot2<T>::dot(x[i], l[i], s0);
+        s1 = Dot2<T>::dot(x[i + 1], l[i + 1], s1);
+      }
+      const float part = (s0 + s1) * am[u][j];
+      acc[j] += valid ? part : 0.0f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) acc[j] = wave_sum(acc[j]);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      const int row = r0 + wave + GC_WAVES * j;
+      if (row < r1) out[row] = Io<T>::from_f32(acc[j]);
+    }
+  }
+}
+
 // General path (any K, ldb, alignment): one wave per row, one element per lane step.
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -300,6 +442,51 @@ k_gemv_4bit_generic(int M, int K, const T* __restrict__ A, const uint8_t* __rest
   if (lane == 0) out[row] = Io<T>::from_f32(acc);
 }
 
+// k_gemv_4bit_cu instance for (U, RMAX) rounded up to an instantiated pair; false when none fits.
+template <typename T, int U, bool NESTED>
+static bool launch_gemv_cu_r(int rmax, int m, int k, const T* A, const uint8_t* B, const GemvStats& st,
+                             const float* datatype, T* out, int ldb, int G, size_t lds) {
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(G), dim3(GC_THREADS), lds, current_stream(), m, k, A, B, st, datatype, out, ldb, G);
+    return true;
+  };
+  if (rmax <= 1) return go(k_gemv_4bit_cu<T, U, 1, NESTED>);
+  if (rmax <= 2) return go(k_gemv_4bit_cu<T, U, 2, NESTED>);
+  if constexpr (U <= 4) {
+    if (rmax <= 3) return go(k_gemv_4bit_cu<T, U, 3, NESTED>);
+    if (rmax <= 4) return go(k_gemv_4bit_cu<T, U, 4, NESTED>);
+  }
+  if constexpr (U <= 2) {
+    if (rmax <= 6) return go(k_gemv_4bit_cu<T, U, 6, NESTED>);
+    if (rmax <= 8) return go(k_gemv_4bit_cu<T, U, 8, NESTED>);
+  }
+  if constexpr (U == 1) {
+    if (rmax <= 12) return go(k_gemv_4bit_cu<T, U, 12, NESTED>);
+    if (rmax <= 16) return go(k_gemv_4bit_cu<T, U, 16, NESTED>);
+  }
+  return false;
+}
+
+template <typename T, bool NESTED>
+static bool launch_gemv_cu(int m, int k, const T* A, const uint8_t* B, const GemvStats& st, const float* datatype,
+                           T* out, int ldb, size_t lds) {
+  const int G = m < 256 ? m : 256;                    // one workgroup per CU
+  const int rows_max = (m + G - 1) / G;
+  const int rmax = (rows_max + GC_WAVES - 1) / GC_WAVES;
+  const int u = ((k >> 5) + 63) / 64;
+  switch (u) {
+    case 1: return launch_gemv_cu_r<T, 1, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
+    case 2: return launch_gemv_cu_r<T, 2, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
+    case 3: return launch_gemv_cu_r<T, 3, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
+    case 4: return launch_gemv_cu_r<T, 4, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
+    case 5: case 6: return launch_gemv_cu_r<T, 6, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
+    case 7: case 8: return launch_gemv_cu_r<T, 8, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
+    default: return false;
+  }
+}
+
+int g_gemv_kernel = 0;   // 0 = auto (k_gemv_4bit_dot), 2 = k_gemv_4bit_cu (A/B benchmarks, tests)
+
 // Launch the table/dot kernel when the shape fits it; false -> caller uses another kernel.
 template <typename T>
 bool launch_gemv_dot(int m, int k, const T* A, const uint8_t* B, GemvStats st, const float* datatype, T* out, int ldb,
@@ -311,6 +498,11 @@ bool launch_gemv_dot(int m, int k, const T* A, const uint8_t* B, GemvStats st, c
   if (k > GV_MAX_K || lds > 65536) return false;
   st.bs_shift = __builtin_ctz(blocksize);
   st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
+  if (g_gemv_kernel == 2) {   // one workgroup per CU: measured slower at 11008 x 4096 (10.4 vs 8.8 us)
+    const bool ok = nested ? launch_gemv_cu<T, true>(m, k, A, B, st, datatype, out, ldb, lds)
+                           : launch_gemv_cu<T, false>(m, k, A, B, st, datatype, out, ldb, lds);
+    if (ok) return true;
+  }
   const int nch = k >> 5;
   auto go = [&](auto kern, int R) {
     const int waves = (m + R - 1) / R;
@@ -365,6 +557,9 @@ void gemv_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* a
 using namespace bnb;
 
 extern "C" {
+
+// [additive, testing] 0 = auto (the 4-waves-x-R-rows kernel), 2 = the one-workgroup-per-CU kernel
+void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
 
 void cgemm_4bit_inference_naive_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax, float* datatype,
                                      fp16_t* out, int lda, int ldb, int ldc, int blocksize) {

@@ -86,6 +86,10 @@ int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bnb_bf16* A, uns
                                            float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2);
 
+/* [additive, testing] GEMV kernel choice: 0 = auto (the 4-waves-x-R-rows kernel), 2 = the one-workgroup-per-CU
+ * kernel (when the layer's weights fit in flight); both give identical bits */
+void cgemv_4bit_set_kernel(int which);
+
 /* ---- 4-bit GEMM (any number of activation rows): ref:sycl/pythonInterface.cpp:377-378 (slot of the
  * broken kgemm_4bit_inference, re-implemented as a fused NF4 GEMM) ----
  * m = out_features, n = activation rows, k = in_features (k % 64 == 0):
@@ -100,8 +104,8 @@ void cgemm_4bit_inference_code_fp16(int m, int n, int k, bnb_fp16* A, unsigned c
 void cgemm_4bit_inference_code_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, float* absmax, float* datatype,
                                     bnb_bf16* out, int lda, int ldb, int ldc, int blocksize);
 /* [additive] the same with a caller-owned fp32 workspace that lets small tile grids (narrow column
- * shards) run split-K on the 256x256 kernel; size it with cgemm_4bit_workspace_bytes (0 = split-K
- * not used for this shape).  A NULL or smaller workspace falls back to the unsplit kernels. */
+ * shards, few tokens) run split-K; size it with cgemm_4bit_workspace_bytes (0 = split-K not used for this
+ * shape).  A NULL or smaller workspace falls back to the unsplit kernels. */
 void cgemm_4bit_inference_code_ws_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, float* absmax,
                                        float* datatype, bnb_fp16* out, int lda, int ldb, int ldc, int blocksize,
                                        float* workspace, long long workspace_bytes);

@@ -442,3 +442,25 @@ def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
     assert torch.equal(F.gemm_4bit(X, q, st), torch.matmul(X, F.dequantize_4bit(q, st).t()))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("shape", [(11008, 4096), (4096, 11008), (4096, 4096), (1024, 8192), (3584, 8192),
+                                   (7, 64), (300, 6144), (257, 16384), (12345, 128), (1, 4096)])
+def test_gemv_cu_kernel_matches_dot_kernel(dev, dtype, nested, shape):
+    """The one-workgroup-per-CU GEMV (balanced row ranges, clamped duplicate rows) gives the bits of the
+    4-waves-x-R-rows kernel on every decode shape (Llama-2-7B / 70B-shard projections, ragged and tiny M)."""
+    F = _F()
+    N, K = shape
+    torch.manual_seed(N + K)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    x = torch.randn(1, K, device=dev, dtype=dtype)
+    y_dot = F.gemv_4bit(x, q.t(), state=st)
+    F.lib.cgemv_4bit_set_kernel(2)
+    try:
+        y_auto = F.gemv_4bit(x, q.t(), state=st)
+    finally:
+        F.lib.cgemv_4bit_set_kernel(0)
+    assert torch.equal(y_auto.view(torch.int16), y_dot.view(torch.int16))
