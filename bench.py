@@ -81,9 +81,22 @@ def bench_int8(dev, m, n, k, iters=20):
         F.igemmlt_dequant(ca, CB, sca, SCB, out=out)
     t_inf = _time_loop(fwd_inference, max(5, iters // 2))
     ops = 2.0 * m * n * k
+    # the reference ABI's own flow (ref:autograd/_functions.py:394-398): A -> col32, B cached as col_turing,
+    # cigemmlt_turing_32 (int32 col32 out), then cdequant_mm_int32_fp16 -- three launches per forward
+    CxB, SB = F.transform(CB, "col_turing")
+    C32A, SA = F.transform(CA, "col32")
+    out32, Sout = F.igemmlt(C32A, CxB, SA, SB)
+    t_tr = _time_loop(lambda: F.transform(CA, "col32"), iters)
+    t_ig = _time_loop(lambda: F.igemmlt(C32A, CxB, SA, SB, out=out32, Sout=Sout), iters)
+    t_mm = _time_loop(lambda: F.mm_dequant(out32, Sout, SCA, SCB, out=out), iters)
+    abi = {"igemmlt_turing_32_us": t_ig * 1e6, "igemmlt_turing_32_tops": ops / t_ig / 1e12,
+           "transform_col32_us": t_tr * 1e6, "mm_dequant_us": t_mm * 1e6,
+           "flow_us": (t_tr + t_ig + t_mm) * 1e6,
+           "note": "F.transform(CA,'col32') + F.igemmlt(C32A, CxB col_turing) + F.mm_dequant, B transformed once"}
     return {"shape": [m, n, k], "tops": ops / t_gemm / 1e12, "us": t_gemm * 1e6,
             "frac_of_int8_peak": ops / t_gemm / 1e12 / PEAK_INT8_TOPS,
-            "forward_with_double_quant_us": t_fwd * 1e6, "forward_inference_row_quant_us": t_inf * 1e6}
+            "forward_with_double_quant_us": t_fwd * 1e6, "forward_inference_row_quant_us": t_inf * 1e6,
+            "reference_abi_path": abi}
 
 
 def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):

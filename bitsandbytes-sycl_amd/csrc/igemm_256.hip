@@ -6,7 +6,8 @@
 // 16x16), BK = 128 bytes, two LDS stages (2 x (32 + 32) KiB), one barrier per k-step, fragments register-
 // pipelined across it.  Both operands
 // arrive by LDS-DMA (16 B per lane, XOR-swizzled through the source address) from any layout whose
-// 16-k runs are contiguous: row-major, col32 (A) and col_ampere (B).  Fragment convention: lane l
+// 16-k runs are contiguous: row-major, col32 (A) and col_ampere (B); col_turing B (4-k runs, the reference's
+// formatB, ref:functional.py:410-418) is copied by whole 8-row groups and its fragments gathered as 4 dwords.  Fragment convention: lane l
 // holds 16 consecutive k of row l&15, k-chunk l>>4 -- identical for A and B, so the int32 result is
 // exact whatever order the instruction sums k in.  Epilogues: int32 row-major / col32, int8 col32
 // (alpha = 1 or per-row scale) and the fused mm_dequant to fp16, staged through LDS for 16-B stores.
@@ -58,12 +59,29 @@ k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __r
     brow[i] = min(n0 + row, N - 1);
     kslot[i] = 16 * ((lane & 7) ^ (row & 7));
   }
+  // col_turing B (col4_4r2_8c, ldb = 32 * pad8(rows)): within a 32-column block the 256 tile rows are 32 groups of
+  // 8 rows x 32 bytes = 8 KiB contiguous, and a 16-B chunk holds 4 bytes (4 consecutive k) of 4 rows.  The tile's
+  // 4 column blocks are copied as they lie (4 x 8 KiB); slot s of (group g, row parity par) receives source chunk
+  // s ^ (2 (g & 1) + par), which makes the fragment reads below conflict-free.  Rows past pad8(n) re-read the last
+  // group (their outputs are not stored).
+  // One lane offset (the lane's group, parity and swizzled chunk; gl & 1 = (lane >> 4) & 1 for every piece); the
+  // piece's column block and 1-KiB slice are wave-uniform.  Offsets are clamped to the buffer (K / 32 column
+  // blocks of ldb bytes, < 4 GiB), so rows past pad8(n) read valid bytes.
+  const unsigned t_lane = ((n0 >> 3) + (lane >> 4)) * 256 + ((lane >> 3) & 1) * 128 +
+                          16 * ((lane & 7) ^ (2 * ((lane >> 4) & 1) + ((lane >> 3) & 1)));
+  const unsigned t_last = (unsigned)((long long)(K >> 5) * ldb - 16);
+  auto dma_b_turing = [&](int kt, int buf, int i) {
+    const int p = 4 * wave + i, cb = p >> 3, j = p & 7;
+    const unsigned off = min(t_lane + (unsigned)(((long long)kt * 4 + cb) * ldb) + 1024u * j, t_last);
+    glds16(B + off, smem + 2 * J_TILE + buf * J_TILE + cb * 8192 + j * 1024);
+  };
   auto dma = [&](int kt, int buf) {
     const long long k0 = (long long)kt * J_BK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       glds16(chunk_ptr<AF>(A, lda, arow[i], k0 + kslot[i]), smem + buf * J_TILE + (4 * wave + i) * 1024);
-      glds16(chunk_ptr<BF>(B, ldb, brow[i], k0 + kslot[i]), smem + 2 * J_TILE + buf * J_TILE + (4 * wave + i) * 1024);
+      if constexpr (BF == TURING) dma_b_turing(kt, buf, i);
+      else glds16(chunk_ptr<BF>(B, ldb, brow[i], k0 + kslot[i]), smem + 2 * J_TILE + buf * J_TILE + (4 * wave + i) * 1024);
     }
   };
 
@@ -78,13 +96,35 @@ k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __r
   // so after the barrier the wave reads tile t+1's ks = 0 fragments under tile t's ks = 1 MFMAs; the
   // barrier and a tile's first LDS latency hide behind 32 MFMAs (tools/igemm_lab.hip: 5-8 % over
   // reading each k-half after the barrier, outputs bit-identical).
+  // col_turing fragment offsets: row r = 64 wn + 16 j + (lane & 15) lies in group 8 wn + 2 j + ((lane >> 3) & 1) at
+  // parity lane & 1 and pair (lane & 7) >> 1; k-chunk (lane >> 4) -> column block (lane >> 5), half (lane >> 4) & 1
+  int tb[4] = {0, 0, 0, 0};
+  if constexpr (BF == TURING) {
+    const int f = 2 * ((lane >> 3) & 1) + (lane & 1);
+    const int base = (8 * wn + ((lane >> 3) & 1)) * 256 + (lane & 1) * 128 + 4 * ((lane & 7) >> 1) +
+                     8192 * (lane >> 5) + 64 * ((lane >> 4) & 1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) tb[u] = base + 16 * (u ^ f);
+  }
   uint4 fa[2][8], fb[2][4];
   auto frag = [&](int buf, int ks, uint4 (&a)[8], uint4 (&b)[4]) {
     const uint8_t* as = smem + buf * J_TILE;
     const uint8_t* bs = smem + 2 * J_TILE + buf * J_TILE;
     const int slot = 4 * ks + (lane >> 4);
+    if constexpr (BF == TURING) {
+      // 16 consecutive k of one row = 4 dwords from the 4 chunks of its (group, parity) half-row, read in k order;
+      // the lane's offsets tb[u] are loop-invariant, k-half ks adds 2 column blocks and fragment j 2 groups
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz(64 * wn + 16 * j + (lane & 15), slot));
+      for (int j = 0; j < 4; ++j) {
+        uint32_t d[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) d[u] = *reinterpret_cast<const uint32_t*>(bs + tb[u] + ks * 16384 + j * 512);
+        b[j] = make_uint4(d[0], d[1], d[2], d[3]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const uint4*>(bs + swz(64 * wn + 16 * j + (lane & 15), slot));
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const uint4*>(as + swz(128 * wm + 16 * i + (lane & 15), slot));
   };
@@ -187,11 +227,12 @@ template <int AF, int BF, int EPI>
 bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale,
                       long long lda, long long ldb, long long ldc, const float* rowStats, const float* colStats,
                       const fp16_t* bias) {
-  if constexpr (AF == TURING || BF == TURING) {
-    return false;                                                  // 4-byte runs: register-staged kernel
+  if constexpr (AF == TURING) {
+    return false;                                                  // A in 4-byte runs: register-staged kernel
   } else {
     if (k % J_BK != 0 || m < 256 || n < 256) return false;
     if ((AF == ROW && lda % 16) || (BF == ROW && ldb % 16) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return false;
+    if (BF == TURING && (ldb % 256 || ldb < 32LL * n || (long long)(k / 32) * ldb >= (1LL << 32))) return false;
     const long long tiles = (long long)((m + J_BM - 1) / J_BM) * ((n + J_BN - 1) / J_BN);
     hipLaunchKernelGGL((k_igemm_256<AF, BF, EPI>), dim3((unsigned)tiles), dim3(J_THREADS), 0, current_stream(), m, n,
                        k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias);

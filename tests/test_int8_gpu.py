@@ -214,3 +214,32 @@ def test_matmul8bitlt_inference_uses_row_quant(dev):
     CA, _, SCA, _, _ = F.double_quant(A)
     exp = F.igemmlt_dequant(CA, st.CB, SCA, st.SCB)
     assert torch.equal(out, exp)
+
+
+@pytest.mark.parametrize("mnk", [(300, 520, 384), (512, 768, 1024), (257, 1000, 128)])
+def test_igemmlt_turing_abi_all_epilogues(dev, mnk):
+    """The reference ABI's own formatB (col_turing, ref:functional.py:410-418) at sizes that take the 256-tile
+    kernel: cigemmlt_turing_32 / _8 / _8_rowscale against the exact oracle, ragged last tiles included."""
+    F = _F()
+    m, n, k = mnk
+    rng = np.random.default_rng(m * 3 + n)
+    A = rng.integers(-127, 128, size=(m, k), dtype=np.int8)
+    B = rng.integers(-127, 128, size=(n, k), dtype=np.int8)
+    At, Bt = torch.from_numpy(A).to(dev), torch.from_numpy(B).to(dev)
+    C32A, SA = F.transform(At, "col32")
+    CxB, SB = F.transform(Bt, "col_turing")
+    out32, _ = F.igemmlt(C32A, CxB, SA, SB)
+    assert np.array_equal(ref.untransform(out32.cpu().numpy(), m, n, "col32"), ref.igemmlt(A, B))
+    small = rng.integers(-3, 4, size=(m, k), dtype=np.int8)
+    C32s, SAs = F.transform(torch.from_numpy(small).to(dev), "col32")
+    out8, _ = F.igemmlt(C32s, CxB, SAs, SB, dtype=torch.int8)
+    assert np.array_equal(ref.untransform(out8.cpu().numpy(), m, n, "col32"), ref.igemmlt_int8_out(small, B))
+    scale = torch.from_numpy(rng.uniform(0.001, 0.01, m).astype(np.float32)).to(dev)
+    out = torch.zeros_like(out8)
+    rc = F.lib.cigemmlt_turing_8_rowscale(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(C32A), F.get_ptr(CxB),
+                                          F.get_ptr(out), F.get_ptr(scale), ct.c_int32(32 * m),
+                                          ct.c_int32(((n + 7) // 8) * 8 * 32), ct.c_int32(32 * m))
+    torch.cuda.synchronize()
+    assert rc == 0
+    got = ref.untransform(out.cpu().numpy(), m, n, "col32")
+    assert np.array_equal(got, ref.igemmlt_int8_out(A, B, scale.cpu().numpy()))
