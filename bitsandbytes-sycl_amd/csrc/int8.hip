@@ -356,10 +356,49 @@ __global__ void k_transform(const int8_t* __restrict__ src, int8_t* __restrict__
   }
 }
 
+// Row-major -> col32 / col_ampere, 16 B per lane: a 16-column run of one row stays contiguous in both formats
+// (c % 32 is the fastest index), so each lane moves one 16-B chunk with one load and one store.  Needs
+// cols % 16 == 0 and 16-B aligned pointers; the padding of the output is not written (the reference's buffers
+// come zero-filled, functional.py:482-518).
+// Lanes walk the OUTPUT in order (consecutive lanes store consecutive 16 B): chunk i = (column block cb, row r,
+// half h) for col32 -- output byte 16 i; for col_ampere the row order inside a 32-row block is the format's
+// interleave, so the lane's source row is found through the inverse map.
+template <int F>
+__global__ void __launch_bounds__(256)
+k_transform16(const int8_t* __restrict__ src, int8_t* __restrict__ dst, int rows, int cols) {
+  const long long rp = (F == COL32) ? rows : pad_to(rows, 32);   // rows held per column block
+  const long long nq = (long long)((cols + 31) >> 5) * rp * 2;   // a half-filled last block skips its h = 1 lanes
+  const long long ld = 32 * rp;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += (long long)gridDim.x * blockDim.x) {
+    const long long cb = i / (2 * rp), rem = i - cb * 2 * rp;
+    const int h = (int)(rem & 1);
+    long long r = rem >> 1;                                   // row slot inside the column block
+    if constexpr (F == AMPERE) {
+      // slot s = 32 (r / 32) + x holds source row 32 (r / 32) + a^-1(x), a(y) = 8 ((y % 8) / 2) + 2 (y / 8) + y % 2
+      const int x = (int)(r & 31);
+      const int y = 8 * ((x >> 1) & 3) + 2 * (x >> 3) + (x & 1);   // the inverse interleave
+      r = (r & ~31LL) + y;
+    }
+    const int c = (int)(32 * cb + 16 * h);
+    if (r >= rows || c >= cols) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(src + r * cols + c);
+    *reinterpret_cast<uint4*>(dst + fmt_offset<F>(r, c, ld)) = v;
+  }
+}
+
 template <int F, bool TRANSPOSE, bool INVERSE>
 static void launch_transform(const int8_t* A, int8_t* out, int rows, int cols) {
   const long long n = (long long)rows * cols;
   if (n <= 0) return;
+  if constexpr ((F == COL32 || F == AMPERE) && !TRANSPOSE && !INVERSE) {
+    if (cols % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+      long long g = (n / 16 + 255) / 256;
+      if (g > 16384) g = 16384;
+      hipLaunchKernelGGL((k_transform16<F>), dim3((unsigned)g), dim3(256), 0, current_stream(), A, out, rows, cols);
+      BNB_LAUNCH_CHECK("transform");
+      return;
+    }
+  }
   long long g = (n + 255) / 256;
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL((k_transform<F, TRANSPOSE, INVERSE>), dim3((unsigned)g), dim3(256), 0, current_stream(), A, out, rows, cols);
@@ -384,6 +423,43 @@ k_dequant_mm_col32(const int32_t* __restrict__ C, const float* __restrict__ rowS
       const int32_t acc = C[(long long)(c >> 5) * 32 * numRows + 32LL * r + (c & 31)];
       out[(long long)r * numCols + c] = mm_dequant_value(acc, rs, colStats[c], bias ? (float)bias[c] : 0.0f);
     }
+  }
+}
+
+// 8 consecutive columns per lane (numCols % 8 == 0, 16-B aligned): two 16-B int32 loads (one col32 run), the
+// column statistics and bias as 16-B loads, one 16-B fp16 store; same per-element arithmetic (mm_dequant_value)
+__global__ void __launch_bounds__(256)
+k_dequant_mm_col32_v8(const int32_t* __restrict__ C, const float* __restrict__ rowStats,
+                      const float* __restrict__ colStats, fp16_t* __restrict__ out, const fp16_t* __restrict__ bias,
+                      int numRows, int numCols) {
+  const int cg = numCols >> 3;
+  const long long groups = (long long)numRows * cg;
+  for (long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(g / cg), c0 = 8 * (int)(g - (long long)r * cg);
+    const int32_t* src = C + (long long)(c0 >> 5) * 32 * numRows + 32LL * r + (c0 & 31);
+    const int4 a0 = reinterpret_cast<const int4*>(src)[0], a1 = reinterpret_cast<const int4*>(src)[1];
+    const float4 s0 = reinterpret_cast<const float4*>(colStats + c0)[0];
+    const float4 s1 = reinterpret_cast<const float4*>(colStats + c0)[1];
+    float bv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (bias) {
+      const uint4 bw = *reinterpret_cast<const uint4*>(bias + c0);
+      const uint32_t w[4] = {bw.x, bw.y, bw.z, bw.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bv[2 * j] = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j] & 0xFFFF));
+        bv[2 * j + 1] = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j] >> 16));
+      }
+    }
+    const float rs = rowStats[r];
+    const int32_t acc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float cs[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = (uint32_t)__builtin_bit_cast(uint16_t, mm_dequant_value(acc[2 * j], rs, cs[2 * j], bv[2 * j])) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, mm_dequant_value(acc[2 * j + 1], rs, cs[2 * j + 1], bv[2 * j + 1]))
+              << 16);
+    *reinterpret_cast<uint4*>(out + (long long)r * numCols + c0) = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -666,6 +742,15 @@ void cdequant_mm_int32_fp16(int* A, float* rowStats, float* colStats, fp16_t* ou
                             float* newcolStats, fp16_t* bias, int numRows, int numCols) {
   (void)newRowStats; (void)newcolStats;   // unused by the reference kernel as well
   if (numRows <= 0 || numCols <= 0) return;
+  if (numCols % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)colStats & 15) == 0 &&
+      ((uintptr_t)bias & 15) == 0) {
+    long long g = ((long long)numRows * (numCols / 8) + 255) / 256;
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL(k_dequant_mm_col32_v8, dim3((unsigned)g), dim3(256), 0, current_stream(), (const int32_t*)A,
+                       rowStats, colStats, out, bias, numRows, numCols);
+    BNB_LAUNCH_CHECK("dequant_mm_int32_fp16");
+    return;
+  }
   const long long groups = (long long)numRows * ((numCols + 3) / 4);
   long long g = (groups + 255) / 256;
   if (g > 16384) g = 16384;

@@ -642,6 +642,12 @@ GEMM_4BIT_DEQUANT_MIN_FEATURES = 1024
 # Up to this many activation rows the C side runs the weight-streaming kernel (gemm4bit_skinny.hip);
 # with nested statistics the Python side calls its one-launch entry point directly.
 GEMM_4BIT_FEW_TOKENS = 32
+# Between GEMM_4BIT_FEW_TOKENS and this many rows, weights at least twice as wide (out features) as deep (in
+# features) also take the library pair: its 64-row tiles cover the wide output where the fused kernel's 256-wide
+# tile grid needs split-K (tools/smallm_sweep.py, profiles/lab/r02_routing.txt, graph replay, us fused vs library:
+# 11008 x 4096 at 64 / 128 / 256 rows 53.8 / 58.8 / 67.5 vs 45.1 / 50.6 / 65.1; 4096 x 4096 27.0 / 31.8 / 35.0 vs
+# 29.5 / 36.0 / 34.0; 4096 x 11008 36.3 / 38.8 / 48.9 vs 52.7 / 71.2 / 64.4).
+GEMM_4BIT_WIDE_MAX_ROWS = 256
 
 _DEQ_WS: dict = {}
 _DEQ_META: dict = {}
@@ -678,7 +684,8 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if not A2.is_contiguous() or A2.data_ptr() % 16:
         A2 = A2.contiguous()
     rows = A2.shape[0]
-    library = rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES
+    library = ((rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES)
+               or (GEMM_4BIT_FEW_TOKENS < rows <= GEMM_4BIT_WIDE_MAX_ROWS and N >= 2 * K))
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
