@@ -281,43 +281,54 @@ k_gemv_4bit_dot(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
   }
 }
 
-// One workgroup per CU (the decode weights of one layer fit in flight at once, <= 16 x 16 B per lane).
-// k_gemv_4bit_dot gives every workgroup 4 waves x R rows, so at 11008 rows the 688 workgroups land 2, 3 or 4
-// per CU and the kernel ends with the most loaded CU; here workgroup g of G = min(256, M) owns the balanced
-// row range [g*M/G, (g+1)*M/G) (43 rows at 11008), so every CU streams the same bytes.
-// Wave w takes rows r0 + w + 8j (j < RMAX), clamped to the range: a clamped row re-reads the range's last row,
-// which the owning wave of the same CU is loading at the same moment (an L2 hit, no extra HBM bytes), and its
-// sum is dropped.  Each lane takes chunks lane + 64u (u < U), clamped the same way.  All RMAX x U weight loads
-// are issued before any is consumed, in consumption order (u outer, rows inner), so the compiler's counted
-// waits retire them one by one.  Same table / dot / statistics arithmetic as k_gemv_4bit_dot (bit-identical).
-constexpr int GC_THREADS = 512, GC_WAVES = GC_THREADS / 64;
+// Balanced-range GEMV (default where it fits, K <= 7680).  Measured at 11008 x 4096 (profiles/lab/
+// r02_gemv_floor.txt): k_gemv_4bit_dot spends ~1/4 of its time before its first dot (its workgroups wait for
+// activations and statistics queued behind other workgroups' weight requests) and is then bound by the
+// table lookups' LDS and VALU issue.  This kernel changes four things, arithmetic unchanged (bit-identical):
+//   * G = 2 x CUs workgroups, workgroup g owns rows [g*M/G, (g+1)*M/G) (22 at 11008): every CU gets the same
+//     work, NW = ceil(rows / R) waves take rows r0 + w + NW*j (j < R);
+//   * the table lookup address is ONE v_perm_b32 of {packed dword, lane byte}: entry e of copy c at byte
+//     256 e + 4 c (32 copies over a 64 KiB span; lanes l and l+32 share copy l & 31, different 32-lane groups),
+//     against shift + mask + or for the 128-B-stride table;
+//   * activations are stored swizzled, 16-B piece q of chunk c at 64 c + 16 ((q + (c >> 2)) & 3), so the
+//     ds_read_b128 of chunks lane + 64u is conflict-free (4-way on the plain layout);
+//   * every wave issues its statistics and activation loads, then a barrier, then its weights: the CU's
+//     request queue holds all of the former ahead of any weight request.
+// LDS: 64 KiB table + 2K activations (+ 1 KiB nested code map): two workgroups per CU up to K = 7680 (7168
+// nested), one workgroup of up to 16 waves per CU above that (K <= 16384).
+constexpr int GB_TABLE_BYTES = 65536;
+constexpr int GB_MAX_WAVES = 16;
+constexpr size_t GB_TWO_PER_CU_LDS = 80 * 1024 - 1024;   // two workgroups per CU with room to spare
 
-template <typename T, int U, int RMAX, bool NESTED>
-__global__ void __launch_bounds__(GC_THREADS, 1)
-k_gemv_4bit_cu(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
-               const float* __restrict__ datatype, T* __restrict__ out, int ldb, int G) {
+template <typename T, int R, int U, bool NESTED>
+__global__ void __launch_bounds__(GB_MAX_WAVES * 64)
+k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
+                const float* __restrict__ datatype, T* __restrict__ out, int ldb, int G) {
   extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
-  uint8_t* table = gsm;                               // GV_TABLE_BYTES
-  uint8_t* xs = gsm + GV_TABLE_BYTES;                 // K * 2 bytes
+  uint8_t* table = gsm;                               // GB_TABLE_BYTES
+  uint8_t* xs = gsm + GB_TABLE_BYTES;                 // K * 2 bytes, swizzled
+  float* code2s = reinterpret_cast<float*>(xs + 2 * K);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NW = blockDim.x >> 6;
   const int r0 = (int)((long long)blockIdx.x * M / G), r1 = (int)((long long)(blockIdx.x + 1) * M / G);
   const int nch = K >> 5;
   const long long two_ldb = 2LL * ldb;
-  auto row_of = [&](int j) { return min(r0 + wave + GC_WAVES * j, r1 - 1); };
+  auto row_of = [&](int j) { return min(r0 + wave + NW * j, r1 - 1); };
   auto chunk_of = [&](int u) { return min(lane + 64 * u, nch - 1); };
 
-  // (1a) block statistics; the 16 code values by scalar loads
+  // (1) code values (scalar), block statistics, activations by LDS-DMA (lane i of the instruction for LDS
+  //     slot i = 16 B fetches the piece that belongs there under the swizzle)
   float dt[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) dt[j] = datatype[j];
-  float am[U][RMAX];
-  uint32_t q8[U][RMAX];
-  float a2[U][RMAX];
+  float am[U][R];
+  uint32_t q8[U][R];
+  float a2[U][R];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
+    for (int j = 0; j < R; ++j) {
       const long long blk = (two_ldb * row_of(j) + 32LL * chunk_of(u)) >> st.bs_shift;
       if constexpr (NESTED) {
         q8[u][j] = st.q8[blk];
@@ -329,61 +340,54 @@ k_gemv_4bit_cu(int M, int K, const T* __restrict__ A, const uint8_t* __restrict_
   float offset = 0.0f, c2 = 0.0f;
   if constexpr (NESTED) {
     offset = *st.offset;
-    c2 = st.code2[threadIdx.x & 255];
+    c2 = st.code2[threadIdx.x & 255];                 // threads past 256 load a duplicate, stored by nobody
   }
-  // (1b) activations by LDS-DMA (1 KiB per wave-instruction)
   const int nx = K >> 3;
-  for (int p = wave; p * 64 < nx; p += GC_WAVES) {
-    const int idx = p * 64 + lane;
-    if (idx < nx) glds16(A + 8 * idx, xs + p * 1024);
+  for (int p = wave; p * 64 < nx; p += NW) {
+    const int i = p * 64 + lane, c = i >> 2;
+    if (i < nx) glds16(A + 8 * (4 * c + (((i & 3) - (c >> 2)) & 3)), xs + p * 1024);
   }
-  // (1c) every weight chunk of this wave, non-temporal, behind the DMA (laundered pointer)
+  __builtin_amdgcn_s_barrier();                       // all statistics / activation requests are out
+  // (2) this wave's weights, non-temporal, consumption order
   uintptr_t bp = (uintptr_t)B;
   asm volatile("" : "+s"(bp)::"memory");
-  uint4 b[U][RMAX];
+  uint4 b[U][R];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
+    for (int j = 0; j < R; ++j) {
       const u32x4_t v =
           __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row_of(j) * ldb + 16LL * chunk_of(u)));
       b[u][j] = make_uint4(v.x, v.y, v.z, v.w);
     }
-  // (2) 32 bank-private copies of the pair table: entry e of copy c at byte 128 e + 4 c (512 threads x 4 stores)
-  static_assert(GC_THREADS == 512, "table fill assumes 512 threads");
-  {
-    const int e_lo = (threadIdx.x >> 3) & 15;         // e & 15 for every store of this thread
-    float lo = dt[0];
+  // (3) table: thread t < 256 writes entry t (32 copies, 16-B stores rotated by t to spread the banks)
+  for (int t = threadIdx.x; t < 256; t += NW * 64) {
+    float hi = dt[0], lo = dt[0];
 #pragma unroll
-    for (int j = 1; j < 16; ++j) lo = e_lo == j ? dt[j] : lo;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = threadIdx.x + k * GC_THREADS;     // 16-B store index: entry i >> 3, copies 4 (i & 7) ..
-      const int e_hi = (i >> 3) >> 4;                 // = 4 k + (tid >> 7)
-      float hi = dt[0];
-#pragma unroll
-      for (int j = 1; j < 16; ++j) hi = e_hi == j ? dt[j] : hi;
-      const uint32_t v = Dot2<T>::pair(hi, lo);
-      *reinterpret_cast<uint4*>(table + (i >> 3) * 128 + 16 * (i & 7)) = make_uint4(v, v, v, v);
+    for (int j = 1; j < 16; ++j) {
+      hi = (t >> 4) == j ? dt[j] : hi;
+      lo = (t & 15) == j ? dt[j] : lo;
     }
+    const uint32_t v = Dot2<T>::pair(hi, lo);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * t + 16 * ((k + t) & 7)) = make_uint4(v, v, v, v);
   }
-  float* code2s = reinterpret_cast<float*>(xs + 2 * K);
   if constexpr (NESTED) {
     if (threadIdx.x < 256) code2s[threadIdx.x] = c2;
+    for (int t = threadIdx.x + NW * 64; t < 256; t += NW * 64) code2s[t] = st.code2[t];   // < 4 waves
   }
-  // (3) activations landed (only this wave's RMAX * U weight loads may be outstanding), table visible
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U * RMAX) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * U) : "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
   if constexpr (NESTED) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < RMAX; ++j) am[u][j] = __fadd_rn(__fmul_rn(code2s[q8[u][j]], a2[u][j]), offset);
+      for (int j = 0; j < R; ++j) am[u][j] = __fadd_rn(__fmul_rn(code2s[q8[u][j]], a2[u][j]), offset);
   }
-  float acc[RMAX];
+  float acc[R];
 #pragma unroll
-  for (int j = 0; j < RMAX; ++j) acc[j] = 0.0f;
+  for (int j = 0; j < R; ++j) acc[j] = 0.0f;
   const uint32_t lane4 = (lane & 31) * 4;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -392,16 +396,17 @@ k_gemv_4bit_cu(int M, int K, const T* __restrict__ A, const uint8_t* __restrict_
     uint32_t x[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint4 v = reinterpret_cast<const uint4*>(xs + 64 * c)[q];
+      const uint4 v = reinterpret_cast<const uint4*>(xs + 64 * c)[(q + (c >> 2)) & 3];
       x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
     }
 #pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
+    for (int j = 0; j < R; ++j) {
       const uint32_t w[4] = {b[u][j].x, b[u][j].y, b[u][j].z, b[u][j].w};
       uint32_t l[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        l[i] = *reinterpret_cast<const uint32_t*>(table + ((((w[i >> 2] >> (8 * (i & 3))) & 0xFF) << 7) | lane4));
+      for (int i = 0; i < 16; ++i)   // byte i & 3 of w[i >> 2] -> address byte 1, lane offset -> address byte 0
+        l[i] = *reinterpret_cast<const uint32_t*>(
+            table + __builtin_amdgcn_perm(w[i >> 2], lane4, 0x0C0C0000u | ((4u + (i & 3)) << 8)));
       float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
@@ -413,11 +418,11 @@ k_gemv_4bit_cu(int M, int K, const T* __restrict__ A, const uint8_t* __restrict_
     }
   }
 #pragma unroll
-  for (int j = 0; j < RMAX; ++j) acc[j] = wave_sum(acc[j]);
+  for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
   if (lane == 0) {
 #pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
-      const int row = r0 + wave + GC_WAVES * j;
+    for (int j = 0; j < R; ++j) {
+      const int row = r0 + wave + NW * j;
       if (row < r1) out[row] = Io<T>::from_f32(acc[j]);
     }
   }
@@ -442,50 +447,67 @@ k_gemv_4bit_generic(int M, int K, const T* __restrict__ A, const uint8_t* __rest
   if (lane == 0) out[row] = Io<T>::from_f32(acc);
 }
 
-// k_gemv_4bit_cu instance for (U, RMAX) rounded up to an instantiated pair; false when none fits.
-template <typename T, int U, bool NESTED>
-static bool launch_gemv_cu_r(int rmax, int m, int k, const T* A, const uint8_t* B, const GemvStats& st,
-                             const float* datatype, T* out, int ldb, int G, size_t lds) {
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(G), dim3(GC_THREADS), lds, current_stream(), m, k, A, B, st, datatype, out, ldb, G);
-    return true;
-  };
-  if (rmax <= 1) return go(k_gemv_4bit_cu<T, U, 1, NESTED>);
-  if (rmax <= 2) return go(k_gemv_4bit_cu<T, U, 2, NESTED>);
-  if constexpr (U <= 4) {
-    if (rmax <= 3) return go(k_gemv_4bit_cu<T, U, 3, NESTED>);
-    if (rmax <= 4) return go(k_gemv_4bit_cu<T, U, 4, NESTED>);
+int g_gemv_kernel = 0;   // 0 = auto (k_gemv_4bit_bal where it fits), 1 = k_gemv_4bit_dot only (A/B, tests)
+
+int device_cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
   }
-  if constexpr (U <= 2) {
-    if (rmax <= 6) return go(k_gemv_4bit_cu<T, U, 6, NESTED>);
-    if (rmax <= 8) return go(k_gemv_4bit_cu<T, U, 8, NESTED>);
-  }
-  if constexpr (U == 1) {
-    if (rmax <= 12) return go(k_gemv_4bit_cu<T, U, 12, NESTED>);
-    if (rmax <= 16) return go(k_gemv_4bit_cu<T, U, 16, NESTED>);
-  }
-  return false;
+  return cus;
 }
 
+// k_gemv_4bit_bal for this shape; false when it does not fit (K > GV_MAX_K, or more than 8 weight loads per
+// lane would be needed to cover the rows).  When two workgroups of NW waves share a CU, an instance above 85
+// VGPRs (R * U > 4: 88-98) is limited to NW <= 8 (4 waves per SIMD, 128 VGPRs).
+// A/B knob: g_gemv_kernel = 10 + R forces at least R rows per wave.
 template <typename T, bool NESTED>
-static bool launch_gemv_cu(int m, int k, const T* A, const uint8_t* B, const GemvStats& st, const float* datatype,
-                           T* out, int ldb, size_t lds) {
-  const int G = m < 256 ? m : 256;                    // one workgroup per CU
-  const int rows_max = (m + G - 1) / G;
-  const int rmax = (rows_max + GC_WAVES - 1) / GC_WAVES;
-  const int u = ((k >> 5) + 63) / 64;
-  switch (u) {
-    case 1: return launch_gemv_cu_r<T, 1, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
-    case 2: return launch_gemv_cu_r<T, 2, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
-    case 3: return launch_gemv_cu_r<T, 3, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
-    case 4: return launch_gemv_cu_r<T, 4, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
-    case 5: case 6: return launch_gemv_cu_r<T, 6, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
-    case 7: case 8: return launch_gemv_cu_r<T, 8, NESTED>(rmax, m, k, A, B, st, datatype, out, ldb, G, lds);
+static bool launch_gemv_bal(int m, int k, const T* A, const uint8_t* B, const GemvStats& st, const float* datatype,
+                            T* out, int ldb) {
+  const size_t lds = GB_TABLE_BYTES + 2 * (size_t)k + (NESTED ? 1024 : 0);
+  if (k > GV_MAX_K) return false;
+  const bool two = lds <= GB_TWO_PER_CU_LDS;
+  const int G = min((two ? 2 : 1) * device_cu_count(), m);
+  const int rows = (m + G - 1) / G;
+  int U = ((k >> 5) + 63) / 64;
+  if (U > 4) U = U <= 6 ? 6 : 8;
+  // measured (tools/gemv_sweep.py): two per CU, plain statistics up to 12 waves; nested up to 8 (at 11008 x 4096
+  // nested, 11 waves x 2 rows runs 9.4 us, 8 waves x 3 rows 8.3 us, the 4-waves-x-R-rows kernel 8.8 us)
+  int max_waves = 16;
+  if (two) max_waves = (NESTED || U * ((rows + 11) / 12) > 4) ? 8 : 12;
+  int R = (rows + max_waves - 1) / max_waves;
+  if (g_gemv_kernel >= 10) R = max(R, g_gemv_kernel - 10);   // A/B: more rows per wave
+  if (R > 4 || R * U > 8) return false;
+  // one workgroup per CU pays off for one row per wave (4096 x 11008: 9.9 vs 12.4 us, 4096 x 14336: 12.3 vs
+  // 13.5) but not for two (8192 x 8192: 12.8 vs 11.5 us for the 4-waves-x-R-rows kernel)
+  if (!two && R > 1) return false;
+  const int nw = (rows + R - 1) / R;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(G), dim3(64 * nw), lds, current_stream(), m, k, A, B, st, datatype, out, ldb, G);
+    return true;
+  };
+  switch (R * 8 + U) {
+    case 8 + 1: return go(k_gemv_4bit_bal<T, 1, 1, NESTED>);
+    case 8 + 2: return go(k_gemv_4bit_bal<T, 1, 2, NESTED>);
+    case 8 + 3: return go(k_gemv_4bit_bal<T, 1, 3, NESTED>);
+    case 8 + 4: return go(k_gemv_4bit_bal<T, 1, 4, NESTED>);
+    case 8 + 6: return go(k_gemv_4bit_bal<T, 1, 6, NESTED>);
+    case 8 + 8: return go(k_gemv_4bit_bal<T, 1, 8, NESTED>);
+    case 16 + 1: return go(k_gemv_4bit_bal<T, 2, 1, NESTED>);
+    case 16 + 2: return go(k_gemv_4bit_bal<T, 2, 2, NESTED>);
+    case 16 + 3: return go(k_gemv_4bit_bal<T, 2, 3, NESTED>);
+    case 16 + 4: return go(k_gemv_4bit_bal<T, 2, 4, NESTED>);
+    case 24 + 1: return go(k_gemv_4bit_bal<T, 3, 1, NESTED>);
+    case 24 + 2: return go(k_gemv_4bit_bal<T, 3, 2, NESTED>);
+    case 32 + 1: return go(k_gemv_4bit_bal<T, 4, 1, NESTED>);
+    case 32 + 2: return go(k_gemv_4bit_bal<T, 4, 2, NESTED>);
     default: return false;
   }
 }
 
-int g_gemv_kernel = 0;   // 0 = auto (k_gemv_4bit_dot), 2 = k_gemv_4bit_cu (A/B benchmarks, tests)
 
 // Launch the table/dot kernel when the shape fits it; false -> caller uses another kernel.
 template <typename T>
@@ -498,9 +520,9 @@ bool launch_gemv_dot(int m, int k, const T* A, const uint8_t* B, GemvStats st, c
   if (k > GV_MAX_K || lds > 65536) return false;
   st.bs_shift = __builtin_ctz(blocksize);
   st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
-  if (g_gemv_kernel == 2) {   // one workgroup per CU: measured slower at 11008 x 4096 (10.4 vs 8.8 us)
-    const bool ok = nested ? launch_gemv_cu<T, true>(m, k, A, B, st, datatype, out, ldb, lds)
-                           : launch_gemv_cu<T, false>(m, k, A, B, st, datatype, out, ldb, lds);
+  if (g_gemv_kernel != 1) {
+    const bool ok = nested ? launch_gemv_bal<T, true>(m, k, A, B, st, datatype, out, ldb)
+                           : launch_gemv_bal<T, false>(m, k, A, B, st, datatype, out, ldb);
     if (ok) return true;
   }
   const int nch = k >> 5;

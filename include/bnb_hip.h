@@ -86,8 +86,8 @@ int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bnb_bf16* A, uns
                                            float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2);
 
-/* [additive, testing] GEMV kernel choice: 0 = auto (the 4-waves-x-R-rows kernel), 2 = the one-workgroup-per-CU
- * kernel (when the layer's weights fit in flight); both give identical bits */
+/* [additive, testing] GEMV kernel choice: 0 = auto (the balanced-range kernel where the shape fits, K <= 7680,
+ * else the 4-waves-x-R-rows kernel), 1 = the 4-waves-x-R-rows kernel only; both give identical bits */
 void cgemv_4bit_set_kernel(int which);
 
 /* ---- 4-bit GEMM (any number of activation rows): ref:sycl/pythonInterface.cpp:377-378 (slot of the

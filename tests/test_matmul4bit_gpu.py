@@ -447,20 +447,24 @@ def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("nested", [False, True])
 @pytest.mark.parametrize("shape", [(11008, 4096), (4096, 11008), (4096, 4096), (1024, 8192), (3584, 8192),
-                                   (7, 64), (300, 6144), (257, 16384), (12345, 128), (1, 4096)])
-def test_gemv_cu_kernel_matches_dot_kernel(dev, dtype, nested, shape):
-    """The one-workgroup-per-CU GEMV (balanced row ranges, clamped duplicate rows) gives the bits of the
-    4-waves-x-R-rows kernel on every decode shape (Llama-2-7B / 70B-shard projections, ragged and tiny M)."""
+                                   (14336, 4096), (28672, 4096), (5000, 7680), (7, 64), (300, 6144), (257, 16384),
+                                   (12345, 128), (1, 4096), (513, 2048), (40000, 1024)])
+@pytest.mark.parametrize("quant", [("nf4", 64), ("fp4", 128), ("nf4", 256)])
+def test_gemv_balanced_kernel_matches_dot_kernel(dev, dtype, nested, shape, quant):
+    """The balanced-range GEMV (k_gemv_4bit_bal: 2 workgroups per CU, perm-addressed table, swizzled activations,
+    clamped duplicate rows) gives the bits of the 4-waves-x-R-rows kernel on every decode shape it takes
+    (Llama-2-7B / Llama-3-8B / 70B-shard projections, ragged and tiny M) and falls back where it does not fit."""
     F = _F()
     N, K = shape
+    qt, bs = quant
     torch.manual_seed(N + K)
     W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
-    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
     x = torch.randn(1, K, device=dev, dtype=dtype)
-    y_dot = F.gemv_4bit(x, q.t(), state=st)
-    F.lib.cgemv_4bit_set_kernel(2)
+    y_auto = F.gemv_4bit(x, q.t(), state=st)
+    F.lib.cgemv_4bit_set_kernel(1)
     try:
-        y_auto = F.gemv_4bit(x, q.t(), state=st)
+        y_dot = F.gemv_4bit(x, q.t(), state=st)
     finally:
         F.lib.cgemv_4bit_set_kernel(0)
     assert torch.equal(y_auto.view(torch.int16), y_dot.view(torch.int16))
