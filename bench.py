@@ -402,7 +402,8 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
     i1, a1, o1 = idx[:n1], absmax[:n1 // BS], W[:n1]
     c1_bytes = n1 + n1 // BS * 4 + n1 * 4
     t_port, t_prod = [], []
-    prod_threads = int(F.lib.cset_cpu_threads(0))
+    # the product CPU path on the job's CPU share (torch's thread count), not every core of the machine
+    prod_threads = int(F.lib.cset_cpu_threads(threads))
     for _ in range(5):
         t0 = time.perf_counter()
         lib.port_dequantize_cpu(vp(code), vp(i1), vp(a1), vp(o1), ct.c_longlong(BS), ct.c_longlong(n1))
@@ -411,6 +412,7 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
         t2 = time.perf_counter()
         t_port.append(t1 - t0)
         t_prod.append(t2 - t1)
+    F.lib.cset_cpu_threads(0)
     tp, tq = statistics.median(t_port), statistics.median(t_prod)
     return {"value": value, "unit": "TFLOP/s", "cores": threads, "kind": "port",
             "sample": f"{len(deq)} reps of: dequantize_cpu (1 thread, as ref:sycl/cpu_ops.cpp:7-14) of W[{N},{K}] "
