@@ -11,9 +11,8 @@ Not provided by this backend (they raise NotImplementedError): the non-blockwise
 """
 from __future__ import annotations
 
-from collections import abc as container_abcs, defaultdict
+from collections import defaultdict
 from copy import deepcopy
-from itertools import chain
 
 import torch
 
@@ -21,56 +20,71 @@ from .. import functional as F
 
 
 class MockArgs:
+    """Attribute view of a config dict (the reference's optimizers read ``self.args.<key>``)."""
+
     def __init__(self, initial_data):
-        for key in initial_data:
-            setattr(self, key, initial_data[key])
+        self.__dict__.update(initial_data)
 
 
 class GlobalOptimManager:
-    """Per-parameter config overrides (ref:optim/optimizer.py:24-110)."""
+    """Process-wide registry of per-parameter optimizer settings (behaviour of ref:optim/optimizer.py:24-110).
+
+    Overrides are recorded against the parameter object (``id(p)``) while a model is being built --
+    ``override_config`` directly, ``register_module_override`` by (module, attribute) resolved at the
+    optimizer's first step -- and re-keyed by (group index, position in group) when parameters are
+    registered, which is the key ``Optimizer8bit.get_config`` looks up.
+    """
     _instance = None
 
     def __init__(self):
         raise RuntimeError("Call get_instance() instead")
 
-    def initialize(self):
-        self.pid2config = {}
-        self.index2config = {}
-        self.optimizer = None
-        self.uses_config_override = False
-        self.module_weight_config_triple = []
-
     @classmethod
     def get_instance(cls):
         if cls._instance is None:
-            cls._instance = cls.__new__(cls)
-            cls._instance.initialize()
+            manager = object.__new__(cls)
+            manager.initialize()
+            cls._instance = manager
         return cls._instance
 
+    def initialize(self):
+        self.pid2config = {}                     # id(parameter) -> {setting: value}
+        self.index2config = {}                   # (group index, parameter index) -> the same dict
+        self.module_weight_config_triple = []    # (module, attribute name, settings), resolved lazily
+        self.optimizer = None
+        self.uses_config_override = False
+
+    @staticmethod
+    def _param_groups(params):
+        params = list(params)
+        if params and isinstance(params[0], dict):
+            return params
+        return [{"params": params}]
+
     def register_parameters(self, params):
-        param_groups = list(params)
-        if not isinstance(param_groups[0], dict):
-            param_groups = [{"params": param_groups}]
-        for group_index, group in enumerate(param_groups):
-            for p_index, p in enumerate(group["params"]):
-                if id(p) in self.pid2config:
-                    self.index2config[(group_index, p_index)] = self.pid2config[id(p)]
+        """Attach the id()-keyed overrides to the (group, position) slots of ``params``."""
+        for gindex, group in enumerate(self._param_groups(params)):
+            for pindex, p in enumerate(group["params"]):
+                settings = self.pid2config.get(id(p))
+                if settings is not None:
+                    self.index2config[(gindex, pindex)] = settings
 
     def override_config(self, parameters, key=None, value=None, key_value_dict=None):
-        self.uses_config_override = True
-        if isinstance(parameters, torch.Tensor):
-            parameters = [parameters]
+        """Override settings for one tensor or an iterable of tensors: ``key``/``value`` for one setting,
+        ``key_value_dict`` for several (not both)."""
         if key is not None and value is not None:
-            assert key_value_dict is None
+            if key_value_dict is not None:
+                raise ValueError("pass either key/value or key_value_dict, not both")
             key_value_dict = {key: value}
-        if key_value_dict is not None:
-            for p in parameters:
-                if id(p) in self.pid2config:
-                    self.pid2config[id(p)].update(key_value_dict)
-                else:
-                    self.pid2config[id(p)] = key_value_dict
+        self.uses_config_override = True
+        if key_value_dict is None:
+            return
+        targets = [parameters] if isinstance(parameters, torch.Tensor) else parameters
+        for p in targets:
+            self.pid2config.setdefault(id(p), {}).update(key_value_dict)
 
     def register_module_override(self, module, param_name, config):
+        """Override settings for ``getattr(module, param_name)``, looked up when the optimizer first steps."""
         self.module_weight_config_triple.append((module, param_name, config))
 
 
@@ -98,44 +112,43 @@ class Optimizer8bit(torch.optim.Optimizer):
         super().__setstate__(state)
 
     def load_state_dict(self, state_dict):
-        """ref:optim/optimizer.py:147-215: tensors keep their dtype when they are 8-bit state."""
-        state_dict = deepcopy(state_dict)
-        groups = self.param_groups
-        saved_groups = state_dict["param_groups"]
+        """Restore a saved state (behaviour of ref:optim/optimizer.py:147-215).  Unlike
+        torch.optim.Optimizer's version, 8-bit state keeps its dtype: tensors named in
+        ``non_castable_tensor_keys`` only move to the parameter's device; other floating tensors take the
+        parameter's dtype; uint8 tensors are left as they are."""
+        saved = deepcopy(state_dict)
+        groups, saved_groups = self.param_groups, saved["param_groups"]
         if len(groups) != len(saved_groups):
             raise ValueError("loaded state dict has a different number of parameter groups")
-        if any(len(g["params"]) != len(s["params"]) for g, s in zip(groups, saved_groups)):
-            raise ValueError("loaded state dict contains a parameter group that doesn't match the size of "
-                             "optimizer's group")
-        id_map = {old_id: p for old_id, p in zip(chain.from_iterable(g["params"] for g in saved_groups),
-                                                 chain.from_iterable(g["params"] for g in groups))}
-
-        def cast(param, value):
-            if isinstance(value, torch.Tensor):
-                if param.is_floating_point() and value.dtype != torch.uint8:
-                    value = value.to(param.dtype)
-                return value
-            if isinstance(value, dict):
-                for k, v in value.items():
-                    value[k] = v.to(param.device) if k in self.non_castable_tensor_keys else cast(param, v)
-                return value
-            if isinstance(value, container_abcs.Iterable):
-                return type(value)(cast(param, v) for v in value)
-            return value
-
+        for group, saved_group in zip(groups, saved_groups):
+            if len(group["params"]) != len(saved_group["params"]):
+                raise ValueError("loaded state dict contains a parameter group that doesn't match the size of "
+                                 "optimizer's group")
+        param_of = {}                            # saved parameter id -> live parameter
+        for group, saved_group in zip(groups, saved_groups):
+            param_of.update(zip(saved_group["params"], group["params"]))
         state = defaultdict(dict)
-        for k, v in state_dict["state"].items():
-            if k in id_map:
-                param = id_map[k]
-                state[param] = cast(param, v)
+        for saved_id, value in saved["state"].items():
+            p = param_of.get(saved_id)
+            if p is None:
+                state[saved_id] = value
             else:
-                state[k] = v
-
-        def update_group(group, new_group):
-            new_group["params"] = group["params"]
-            return new_group
-        param_groups = [update_group(g, ng) for g, ng in zip(groups, saved_groups)]
+                state[p] = self._restore_state_value(p, value)
+        param_groups = [dict(saved_group, params=group["params"]) for group, saved_group in zip(groups, saved_groups)]
         self.__setstate__({"state": state, "param_groups": param_groups})
+
+    def _restore_state_value(self, p, value, key=None):
+        if isinstance(value, torch.Tensor):
+            if key in self.non_castable_tensor_keys:
+                return value.to(p.device)
+            if p.is_floating_point() and value.dtype != torch.uint8:
+                return value.to(p.dtype)
+            return value
+        if isinstance(value, dict):
+            return {k: self._restore_state_value(p, v, k) for k, v in value.items()}
+        if isinstance(value, (list, tuple)):
+            return type(value)(self._restore_state_value(p, v) for v in value)
+        return value
 
     def to_gpu(self):
         for group in self.param_groups:
@@ -146,16 +159,19 @@ class Optimizer8bit(torch.optim.Optimizer):
                             self.state[p][k] = v.to(p.device)
 
     def check_overrides(self):
+        """Resolve register_module_override entries: the first slot holding that module attribute's tensor
+        takes the settings."""
+        slots = {}
+        for gindex, group in enumerate(self.param_groups):
+            for pindex, p in enumerate(group["params"]):
+                slots.setdefault(id(p), (gindex, pindex))
         for module, attr, config in self.mng.module_weight_config_triple:
-            pmodule = getattr(module, attr)
-            assert pmodule is not None
-            found = False
-            for gindex, group in enumerate(self.param_groups):
-                for pindex, p in enumerate(group["params"]):
-                    if not found and id(p) == id(pmodule):
-                        self.mng.pid2config[id(p)] = config
-                        self.mng.index2config[(gindex, pindex)] = self.mng.pid2config[id(p)]
-                        found = True
+            target = getattr(module, attr)
+            assert target is not None
+            slot = slots.get(id(target))
+            if slot is not None:
+                self.mng.pid2config[id(target)] = config
+                self.mng.index2config[slot] = config
 
     @torch.no_grad()
     def step(self, closure=None):

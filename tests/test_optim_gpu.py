@@ -211,3 +211,27 @@ def test_small_params_use_fp32_state_and_training_runs(dev):
     st = opt.state[model[0].weight]
     assert st["state1"].dtype == torch.uint8 and st["absmax1"].numel() == (784 * 256 + 2047) // 2048
     assert opt.state[model[0].bias]["state1"].dtype == torch.float32      # 256 < min_8bit_size
+
+
+def test_global_manager_override_changes_state_kind(dev):
+    """GlobalOptimManager: a 32-bit optimizer with one parameter overridden to 8-bit state keeps uint8
+    blockwise state for that parameter only, and its update equals Adam8bit's on the same input."""
+    import python_src_quants as bnb
+    mng = bnb.optim.GlobalOptimManager.get_instance()
+    mng.initialize()
+    torch.manual_seed(3)
+    p1, p2 = (torch.nn.Parameter(torch.randn(8192, device=dev) * 0.1) for _ in range(2))
+    ref = torch.nn.Parameter(p2.detach().clone())
+    mng.override_config(p2, "optim_bits", 8)
+    mng.register_parameters([p1, p2])
+    opt = bnb.optim.Adam([p1, p2], lr=1e-3)
+    opt_ref = bnb.optim.Adam8bit([ref], lr=1e-3)
+    for _ in range(3):
+        g = torch.randn_like(p2) * 0.01
+        p1.grad, p2.grad, ref.grad = torch.randn_like(p1) * 0.01, g.clone(), g.clone()
+        opt.step()
+        opt_ref.step()
+    assert opt.state[p1]["state1"].dtype == torch.float32
+    assert opt.state[p2]["state1"].dtype == torch.uint8
+    assert torch.equal(p2.detach(), ref.detach())
+    mng.initialize()
