@@ -119,7 +119,7 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
             s0, e0 = _events()
             s0.record()
         if world > 1:
-            lin.forward(A, assemble=False, chunks=chunks)
+            lin.forward(A, assemble=True, chunks=chunks)
         else:
             lin.forward_local(A)
         if record:
@@ -150,7 +150,7 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
     return {"shape": [m, n, k], "n_gpus": world, "tops": ops / per / 1e12, "ms_per_step": per * 1e3,
             "median_step_ms_rank0": med * 1e3,
             "step": "int8_row_quant(X) + fused igemmlt+dequant on this rank's CB rows" +
-                    (f" + RCCL all_gather ({chunks} chunks)" if world > 1 else ""),
+                    (f" + RCCL all_gather ({chunks} chunks) + [M, N] assembly" if world > 1 else ""),
             "frac_of_int8_peak": ops / per / 1e12 / PEAK_INT8_TOPS}
 
 
@@ -498,6 +498,8 @@ def main():
     chunks = args.chunks if (world > 1 and args.chunks >= 1 and M % args.chunks == 0) else 1
     Mc = M // chunks
     gathered = torch.empty(chunks, world, Mc, shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
+    # N > 1: the step ends with the layer's [M, N] output assembled (chunk by chunk, as each gather lands)
+    full_out = torch.empty(M, world * shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
     kev = []
 
     library = gemm_kernel_name(Mc, shard).startswith("hipBLASLt")
@@ -522,7 +524,7 @@ def main():
             return r
         if world > 1:
             # chunk c's RCCL all-gather (own stream) overlaps chunk c+1's GEMM; all waited at the end
-            sharded_forward_overlapped(X, mm, world, None, chunks, out=gathered, y=Y)
+            sharded_forward_overlapped(X, mm, world, None, chunks, out=gathered, y=Y, rows_out=full_out)
         else:
             mm(X, Y)
         if record:
@@ -618,7 +620,8 @@ def main():
                                    f"{F.GEMM_4BIT_DEQUANT_MIN_ROWS} rows / {F.GEMM_4BIT_DEQUANT_MIN_FEATURES} features) + bf16 all-gather of output-column shards",
                        "M": M, "N": N, "K": K, "blocksize": BS, "quant_type": "nf4", "compress_statistics": True,
                        "parallelism": (f"column-shard x{world} + RCCL all_gather, {chunks} token-row chunks "
-                                       "(chunk c's all-gather overlaps chunk c+1's GEMM)") if world > 1 else "single GPU"},
+                                       "(chunk c's all-gather overlaps chunk c+1's GEMM; the step ends with the [M, N] "
+                                       "output assembled)") if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                          "kernel": gemm_kernel_name(Mc, shard), "kernel_us": round(kern_s * 1e6, 2),

@@ -580,7 +580,7 @@ using namespace bnb;
 
 extern "C" {
 
-// [additive, testing] 0 = auto (the 4-waves-x-R-rows kernel), 2 = the one-workgroup-per-CU kernel
+// [additive, testing] 0 = auto (k_gemv_4bit_bal where it fits), 1 = the 4-waves-x-R-rows kernel only
 void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
 
 void cgemm_4bit_inference_naive_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax, float* datatype,
@@ -597,7 +597,8 @@ void cgemm_4bit_inference_naive_fp32(int m, int n, int k, float* A, unsigned cha
 }
 
 // Decode GEMV with compressed statistics decoded in-kernel (replaces the dequantize_blockwise launch of
-// functional.py:1982-1984 + the gemv).  Returns 0 when launched, 1 when the shape needs the two-step path.
+// functional.py:1982-1984 + the gemv).  Returns 0 when launched, 1 when the shape needs the two-step path, 2 when
+// the launch failed (also recorded for cget_last_error), so a caller may skip the error query on 0.
 int cgemm_4bit_inference_naive_nested_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, unsigned char* absmax_q,
                                            float* code2, float* absmax2, float* offset, float* datatype, fp16_t* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2) {
@@ -605,7 +606,8 @@ int cgemm_4bit_inference_naive_nested_fp16(int m, int n, int k, fp16_t* A, unsig
   GemvStats st{nullptr, absmax_q, code2, absmax2, offset, 0, 0};
   if (m <= 0) return 0;
   if (!launch_gemv_dot<fp16_t>(m, k, A, B, st, datatype, out, ldb, blocksize, blocksize2)) return 1;
-  BNB_LAUNCH_CHECK("gemv_4bit_nested");
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error((int)e, "gemv_4bit_nested"); return 2; }
   return 0;
 }
 int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, unsigned char* absmax_q,
@@ -615,7 +617,8 @@ int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bf16_t* A, unsig
   GemvStats st{nullptr, absmax_q, code2, absmax2, offset, 0, 0};
   if (m <= 0) return 0;
   if (!launch_gemv_dot<bf16_t>(m, k, A, B, st, datatype, out, ldb, blocksize, blocksize2)) return 1;
-  BNB_LAUNCH_CHECK("gemv_4bit_nested");
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error((int)e, "gemv_4bit_nested"); return 2; }
   return 0;
 }
 

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as ct
 import threading
+import weakref
 from functools import reduce
 import operator
 from typing import Any, Dict, Optional, Tuple
@@ -189,9 +190,12 @@ def _offset_on(state, device) -> Tensor:
     return off.to(device=device, dtype=torch.float32).reshape(1)
 
 
+_get_device = getattr(torch._C, "_cuda_getDevice", None) or torch.cuda.current_device
+
+
 def pre_call(device):
     """Select the device (ref:functional.py:461-464) and bind the library to torch's current stream."""
-    prev_device = torch.cuda.current_device()
+    prev_device = _get_device()
     idx = device.index if isinstance(device, torch.device) else device
     if idx is None:
         idx = prev_device
@@ -205,7 +209,7 @@ def pre_call(device):
 
 
 def post_call(prev_device):
-    if torch.cuda.current_device() != prev_device:
+    if _get_device() != prev_device:
         torch.cuda.set_device(prev_device)
     err = lib.cget_last_error()
     if err:
@@ -558,44 +562,123 @@ def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, absmax:
 
 
 # ----------------------------------------------------------------------------- 4-bit matmul
+class _GemvPlan:
+    """The per-weight part of a decode GEMV call, prepared once: the entry point (with ctypes argtypes, so
+    plain ints pass without wrapper objects), the statistics pointers and the integer arguments.  It holds
+    the statistics tensors it points at and is used only while the state still holds the same objects."""
+    __slots__ = ("fn", "nested", "absmax", "code", "s2", "s2absmax", "s2code", "offset_src", "offset", "dev", "m",
+                 "head", "mid", "tail")
+
+    def valid(self, state, dev) -> bool:
+        if self.dev != dev or self.absmax is not state.absmax or self.code is not state.code:
+            return False
+        if not self.nested:
+            return state.state2 is None
+        s2 = state.state2
+        return (s2 is self.s2 and s2.absmax is self.s2absmax and s2.code is self.s2code
+                and state.offset is self.offset_src)
+
+
+# id(state) -> (weak reference to the state, {(dtype, device): plan}); the entry leaves with the state
+# (QuantState defines __eq__ and so is unhashable: keyed by id, checked by identity)
+_GEMV_PLANS: Dict[int, Tuple[Any, Dict]] = {}
+_I32, _PTR = ct.c_int32, ct.c_void_p
+
+
+def _gemv_plan(A: Tensor, state) -> Optional[_GemvPlan]:
+    """Build (or fetch) the cached plan for a bf16/fp16 decode GEMV against `state`; None when the call
+    needs the general path (fp32 activations, an fp32 absmax that must be decoded first)."""
+    names = {torch.float16: "fp16", torch.bfloat16: "bf16"}
+    if A.dtype not in names:
+        return None
+    dev = A.get_device()
+    entry = _GEMV_PLANS.get(id(state))
+    per_state = entry[1] if entry is not None and entry[0]() is state else None
+    key = (A.dtype, dev)
+    if per_state is not None:
+        plan = per_state.get(key)
+        if plan is not None and plan.valid(state, dev):
+            return plan
+    m, k = state.shape[0], state.shape[1]
+    plan = _GemvPlan()
+    plan.dev, plan.m, plan.absmax, plan.code = dev, m, state.absmax, state.code
+    plan.nested = A.dtype != torch.float32 and _nested_stats_in_kernel_ok(state)
+    ldb, ldm = (k + 1) // 2, m
+    if plan.nested:
+        s2 = state.state2
+        plan.s2, plan.s2absmax, plan.s2code = s2, s2.absmax, s2.code
+        plan.offset_src, plan.offset = state.offset, _offset_on(state, A.device)
+        is_on_gpu([state.absmax, s2.absmax, s2.code, plan.offset, state.code])
+        plan.fn = getattr(lib, f"cgemm_4bit_inference_naive_nested_{names[A.dtype]}")
+        plan.fn.argtypes = [_I32] * 3 + [_PTR] * 8 + [_I32] * 5
+        plan.head = (m, 1, k)
+        plan.mid = (state.absmax.data_ptr(), s2.code.data_ptr(), s2.absmax.data_ptr(), plan.offset.data_ptr(),
+                    state.code.data_ptr())
+        plan.tail = (ldm, ldb, ldm, state.blocksize, s2.blocksize)
+    else:
+        if state.state2 is not None or state.absmax.dtype != torch.float32:
+            return None                      # compressed statistics the kernel cannot decode: general path
+        plan.s2 = plan.s2absmax = plan.s2code = plan.offset_src = plan.offset = None
+        is_on_gpu([state.absmax, state.code])
+        plan.fn = getattr(lib, f"cgemm_4bit_inference_naive_{names[A.dtype]}")
+        plan.fn.argtypes = [_I32] * 3 + [_PTR] * 5 + [_I32] * 4
+        plan.head = (m, 1, k)
+        plan.mid = (state.absmax.data_ptr(), state.code.data_ptr())
+        plan.tail = (ldm, ldb, ldm, state.blocksize)
+    if per_state is None:
+        sid = id(state)
+        per_state = {}
+        _GEMV_PLANS[sid] = (weakref.ref(state, lambda _r, sid=sid: _GEMV_PLANS.pop(sid, None)), per_state)
+    per_state[key] = plan
+    return plan
+
+
+def _gemv_out(A: Tensor, bout: int) -> Tensor:
+    if len(A.shape) == 3:
+        return torch.empty(size=(A.shape[0], A.shape[1], bout), dtype=A.dtype, device=A.device)
+    return torch.empty(size=(A.shape[0], bout), dtype=A.dtype, device=A.device)
+
+
 def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=False, transposed_B=False,
               state=None):
-    """4-bit GEMV for a single activation row (ref:functional.py:1961-2060)."""
-    prev_device = pre_call(A.device)
+    """4-bit GEMV for a single activation row (ref:functional.py:1961-2060).
+
+    bf16/fp16 calls against the same weight reuse a prepared plan (_gemv_plan), so the host cost per call is
+    the checks below, the output allocation, the stream binding and one ctypes call."""
     if state is None:
         raise ValueError("state cannot None. gem_4bit( ) requires the state from quantize_4bit( )")
     if A.numel() != A.shape[-1]:
         raise ValueError(
             'Dimensions of A are invalid. Must be a vector with the leading dimensions of "1", e.g. [1, 1, 2048]',
         )
+    if B.dtype not in (torch.uint8, torch.bfloat16, torch.float16, torch.float32):
+        raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
+    plan = _gemv_plan(A, state) if A.is_cuda else None
+    if plan is not None and B.is_cuda and B.get_device() == plan.dev:
+        if out is None:
+            out = _gemv_out(A, plan.m)
+        elif not out.is_cuda or out.get_device() != plan.dev:
+            is_on_gpu([A, out])
+        prev_device = pre_call(A.device)
+        rc = plan.fn(*plan.head, A.data_ptr(), B.data_ptr(), *plan.mid, out.data_ptr(), *plan.tail)
+        if plan.nested and rc == 0:          # launched, no error recorded (2 = launch error, 1 = declined)
+            if prev_device != plan.dev:
+                torch.cuda.set_device(prev_device)
+            return out
+        if rc != 1 or not plan.nested:
+            post_call(prev_device)
+            return out
+        torch.cuda.set_device(prev_device)   # nested shape the kernel declined: general path below
+    prev_device = pre_call(A.device)
     Bshape = state.shape
     bout = Bshape[0]
     if out is None:
-        if len(A.shape) == 3:
-            out = torch.empty(size=(A.shape[0], A.shape[1], bout), dtype=A.dtype, device=A.device)
-        else:
-            out = torch.empty(size=(A.shape[0], bout), dtype=A.dtype, device=A.device)
+        out = _gemv_out(A, bout)
     m, n, k = Bshape[0], 1, Bshape[1]
     lda, ldc, ldb = Bshape[0], Bshape[0], (A.shape[-1] + 1) // 2
-    if B.dtype not in [torch.uint8, torch.bfloat16, torch.float16, torch.float32]:
-        raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
     names = {torch.float16: "fp16", torch.bfloat16: "bf16", torch.float32: "fp32"}
     if A.dtype not in names:
         raise NotImplementedError(f"Matmul not implemented for data type {A.dtype}")
-    if A.dtype != torch.float32 and _nested_stats_in_kernel_ok(state):
-        # compressed statistics decoded inside the GEMV kernel: one launch instead of
-        # dequantize_blockwise + gemv (ref:functional.py:1982-1984)
-        s2 = state.state2
-        offset = _offset_on(state, A.device)
-        is_on_gpu([B, A, out, state.absmax, s2.absmax, s2.code, offset, state.code])
-        fn = getattr(lib, f"cgemm_4bit_inference_naive_nested_{names[A.dtype]}")
-        rc = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A), get_ptr(B), get_ptr(state.absmax),
-                get_ptr(s2.code), get_ptr(s2.absmax), get_ptr(offset), get_ptr(state.code), get_ptr(out),
-                ct.c_int32(lda), ct.c_int32(ldb), ct.c_int32(ldc), ct.c_int32(state.blocksize),
-                ct.c_int32(s2.blocksize))
-        if rc == 0:
-            post_call(prev_device)
-            return out
     absmax = _absmax_fp32(state)
     is_on_gpu([B, A, out, absmax, state.code])
     fn = getattr(lib, f"cgemm_4bit_inference_naive_{names[A.dtype]}")

@@ -107,12 +107,15 @@ def _gather_async(out: torch.Tensor, y: torch.Tensor, group=None):
 
 
 def sharded_forward_overlapped(x2: torch.Tensor, local_mm: Callable, world: int, group=None, chunks: int = 2,
-                               out: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None) -> torch.Tensor:
+                               out: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None,
+                               rows_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Token-row-chunked sharded forward: the local GEMM of chunk c+1 runs while the all-gather of
     chunk c is in flight (RCCL runs on its own stream; async_op handles order it after the GEMM that
     produced the chunk and before the caller's next use).  local_mm(x_chunk, y_chunk_or_None) returns
     this rank's [Mc, n] slice.  Returns [chunks, world, Mc, n] (chunk c = token rows c*Mc .. +Mc);
-    `chunked_to_rows` assembles [M, world*n].  chunks must divide M (else a single chunk is used)."""
+    `chunked_to_rows` assembles [M, world*n].  chunks must divide M (else a single chunk is used).
+    rows_out ([M, world*n]): assemble there as well, chunk by chunk as each gather lands, so chunk c's
+    copy overlaps chunk c+1's gather; returns rows_out then."""
     M = x2.shape[0]
     if chunks < 1 or M % chunks:
         chunks = 1
@@ -127,8 +130,14 @@ def sharded_forward_overlapped(x2: torch.Tensor, local_mm: Callable, world: int,
             out[c, 0].copy_(yc)
         else:
             works.append(_gather_async(out[c], yc.contiguous(), group))
-    for w in works:
+    for c, w in enumerate(works):
         w.wait()
+        if rows_out is not None:
+            rows_out[c * Mc:(c + 1) * Mc].view(Mc, world, -1).copy_(out[c].permute(1, 0, 2))
+    if rows_out is not None:
+        if world == 1:
+            rows_out.copy_(out.reshape(rows_out.shape))
+        return rows_out
     return out
 
 
@@ -196,8 +205,10 @@ class ColumnShardedLinear4bit(torch.nn.Module):
                 r = F.gemm_4bit(xc, self.qweight, self.quant_state, out=yc, reuse_weight=not first[0])
                 first[0] = False
                 return r
-            g = sharded_forward_overlapped(x2, mm, self.world, self.group, chunks)
-            return chunked_to_rows(g) if assemble else g
+            if not assemble:
+                return sharded_forward_overlapped(x2, mm, self.world, self.group, chunks)
+            rows = torch.empty((x2.shape[0], self.out_features), dtype=x2.dtype, device=x2.device)
+            return sharded_forward_overlapped(x2, mm, self.world, self.group, chunks, rows_out=rows)
         g = gather_columns(self.forward_local(x), self.world, self.group)
         return gathered_to_rows(g) if assemble else g
 
@@ -236,8 +247,10 @@ class ColumnShardedLinear8bitLt(torch.nn.Module):
     def forward(self, x: torch.Tensor, assemble: bool = True, chunks: int = 1) -> torch.Tensor:
         x2 = x.reshape(-1, self.in_features)
         if chunks > 1:
-            g = sharded_forward_overlapped(x2, lambda xc, yc: self.forward_local(xc, yc), self.world, self.group,
-                                           chunks)
-            return chunked_to_rows(g) if assemble else g
+            mm = lambda xc, yc: self.forward_local(xc, yc)  # noqa: E731
+            if not assemble:
+                return sharded_forward_overlapped(x2, mm, self.world, self.group, chunks)
+            rows = torch.empty((x2.shape[0], self.out_features), dtype=torch.float16, device=x2.device)
+            return sharded_forward_overlapped(x2, mm, self.world, self.group, chunks, rows_out=rows)
         g = gather_columns(self.forward_local(x2), self.world, self.group)
         return gathered_to_rows(g) if assemble else g

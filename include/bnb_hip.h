@@ -78,7 +78,8 @@ void cgemm_4bit_inference_naive_fp32(int m, int n, int k, float* A, unsigned cha
 /* Additive: the same GEMV with compressed statistics (compress_statistics=True) decoded in-kernel,
  * absmax[j] = code2[absmax_q[j]] * absmax2[j / blocksize2] + *offset (fp32), replacing the
  * dequantize_blockwise launch of ref:python_src_quants/functional.py:1982-1984.  `offset` is a device
- * pointer to one float.  Returns 0 when launched, 1 when the shape needs the two-step path. */
+ * pointer to one float.  Returns 0 when launched, 1 when the shape needs the two-step path, 2 when the
+ * launch failed (the error is also recorded for cget_last_error). */
 int cgemm_4bit_inference_naive_nested_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, unsigned char* absmax_q,
                                            float* code2, float* absmax2, float* offset, float* datatype, bnb_fp16* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2);
@@ -86,8 +87,8 @@ int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bnb_bf16* A, uns
                                            float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2);
 
-/* [additive, testing] GEMV kernel choice: 0 = auto (the balanced-range kernel where the shape fits, K <= 7680,
- * else the 4-waves-x-R-rows kernel), 1 = the 4-waves-x-R-rows kernel only; both give identical bits */
+/* [additive, testing] GEMV kernel choice: 0 = auto (the balanced-range kernel where the shape fits, else the
+ * 4-waves-x-R-rows kernel), 1 = the 4-waves-x-R-rows kernel only; both give identical bits */
 void cgemv_4bit_set_kernel(int which);
 
 /* ---- 4-bit GEMM (any number of activation rows): ref:sycl/pythonInterface.cpp:377-378 (slot of the

@@ -468,3 +468,35 @@ def test_gemv_balanced_kernel_matches_dot_kernel(dev, dtype, nested, shape, quan
     finally:
         F.lib.cgemv_4bit_set_kernel(0)
     assert torch.equal(y_auto.view(torch.int16), y_dot.view(torch.int16))
+
+
+@pytest.mark.parametrize("nested", [False, True])
+def test_gemv_plan_cache_follows_state_changes(dev, nested):
+    """gemv_4bit's cached per-weight call plan: repeated calls give identical bits, and replacing the state's
+    statistics (absmax, nested offset) or calling with another dtype is seen on the next call."""
+    F = _F()
+    torch.manual_seed(5)
+    N, K = 1024, 2048
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    x = torch.randn(1, K, device=dev, dtype=torch.bfloat16)
+    y0 = F.gemv_4bit(x, q.t(), state=st)
+    assert torch.equal(F.gemv_4bit(x, q.t(), state=st), y0)
+    if nested:
+        st.offset = st.offset * 2 if torch.is_tensor(st.offset) else st.offset * 2
+        F.lib.cgemv_4bit_set_kernel(1)
+        try:
+            exp = F.gemv_4bit(x, q.t(), state=st)
+        finally:
+            F.lib.cgemv_4bit_set_kernel(0)
+        y1 = F.gemv_4bit(x, q.t(), state=st)
+        assert torch.equal(y1, exp) and not torch.equal(y1, y0)
+    else:
+        st.absmax = st.absmax * 2
+        y1 = F.gemv_4bit(x, q.t(), state=st)
+        assert torch.equal(y1.float(), (y0.float() * 2).to(torch.bfloat16).float()) or \
+            torch.allclose(y1.float(), y0.float() * 2, rtol=1e-2, atol=1e-3)
+    yh = F.gemv_4bit(x.half(), q.t(), state=st)
+    assert yh.dtype == torch.float16 and torch.allclose(yh.float(), y1.float(), rtol=2e-2, atol=2e-2)
+    out = torch.empty(1, N, device=dev, dtype=torch.bfloat16)
+    assert F.gemv_4bit(x, q.t(), state=st, out=out) is out and torch.equal(out, y1)

@@ -100,6 +100,9 @@ def _worker_overlap(rank, world, port, ret):
             g = sharded_forward_overlapped(torch.from_numpy(X), local_mm, world, chunks=chunks)
             ok &= g.shape[0] == (chunks if M % chunks == 0 else 1)
             ok &= bool(np.array_equal(chunked_to_rows(g).numpy(), exp))
+            full = torch.full((M, N), float("nan"))
+            r = sharded_forward_overlapped(torch.from_numpy(X), local_mm, world, chunks=chunks, rows_out=full)
+            ok &= r is full and bool(np.array_equal(full.numpy(), exp))
         ret[rank] = ok
     finally:
         dist.destroy_process_group()

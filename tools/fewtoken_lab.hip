@@ -1,0 +1,227 @@
+// Few-token NF4 GEMM lab, round 2: the library kernel (k_gemm_4bit_skinny: A = dequantised weight rows via a
+// single-copy float2 table + packed multiply + cast) against k_ft, which feeds the weights as the MFMA B operand
+// straight from a conflict-free bf16 pair table {T(code[hi]), T(code[lo])} (32 copies, GEMV layout) and scales
+// each 64-k step's MFMA sum by the lane's own absmax (D[token][row]: a lane holds one weight row).
+// 8 tokens x 11008 x 4096 by default (argv: N K M), 14 rotating weight copies, plain fp32 absmax.
+#include "gemm4bit_skinny.hip"
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <vector>
+namespace bnb {
+hipStream_t current_stream() { return nullptr; }
+void set_error(int, const char* what) { printf("error: %s\n", what); }
+}  // namespace bnb
+using namespace bnb;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+typedef const __attribute__((address_space(1))) uint8_t* gb_t;
+typedef unsigned int u32x2v_t __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) u32x2v_t* gv2_t;
+constexpr int FT_TABLE = 256 * 128;   // max over the copy counts
+
+template <typename T> struct Pair;
+template <> struct Pair<bf16_t> {
+  __device__ static uint32_t make(float lo, float hi) { return pack_bf16x2(lo, hi); }
+};
+
+// NS steps of 64 k per split; MT token tiles of 16.
+template <typename T, int MT, int NS, int C = 32>
+__global__ void __launch_bounds__(256, 2)
+k_ft(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
+     const float* __restrict__ absmax, const float* __restrict__ code, float* __restrict__ ws, T* __restrict__ out,
+     int ldc, int nsplit) {
+  constexpr int MP = 16 * MT;
+  constexpr int ROWB = NS * 128;                       // LDS bytes of one token row's K slice
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  uint8_t* table = sm;
+  uint8_t* xs = sm + 256 * 4 * C;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rb = blockIdx.x / nsplit, split = blockIdx.x - rb * nsplit;
+  const int j = lane & 15, c = lane >> 4;
+  const int row = min(rb * 64 + 16 * wave + j, N - 1);
+  const int s0 = split * NS;                            // first 64-k step of this split
+  const int ns = min(NS, (K >> 6) - s0);
+  float dt[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dt[i] = code[i];
+  // (1) statistics: one absmax per step (bs 64) for this lane's row
+  float am[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) am[s] = absmax[((long long)row * K + 64LL * (s0 + min(s, ns - 1))) >> 6];
+  // (2) activations by LDS-DMA: LDS slot i (16 B) of token row t holds logical slot (i & ~15) | ((i ^ t) & 15)
+  constexpr int SLOTS = MP * NS * 8;
+  for (int p = wave; p * 64 < SLOTS; p += 4) {
+    const int i = p * 64 + lane;
+    const int t = i / (NS * 8), ph = i - t * (NS * 8);
+    const int lg = (ph & ~15) | ((ph ^ t) & 15);
+    const int step = lg >> 3;
+    if (step < ns) glds16(A + (long long)min(t, M - 1) * lda + 64LL * s0 + 8 * lg, xs + p * 1024);
+    else *reinterpret_cast<uint4*>(xs + 16 * i) = make_uint4(0, 0, 0, 0);
+  }
+  // (3) weights: 8 B per step (16 k of row `row`, k = 64 s + 16 c)
+  uintptr_t bp = (uintptr_t)B;
+  asm volatile("" : "+s"(bp)::"memory");
+  uint2 w[NS];
+  const gb_t wp = (gb_t)bp + (long long)row * ldb + 32LL * s0 + 8 * c;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const u32x2v_t v = __builtin_nontemporal_load((gv2_t)(wp + 32 * min(s, ns - 1)));
+    w[s] = make_uint2(v.x, v.y);
+  }
+  // (4) table: entry e copy q at 4 (C e + q)
+  for (int i = tid; i < 256 * C / 4; i += 256) {
+    const int e = i / (C / 4);
+    float hi = dt[0], lo = dt[0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) { hi = (e >> 4) == q ? dt[q] : hi; lo = (e & 15) == q ? dt[q] : lo; }
+    const uint32_t v = Pair<T>::make(hi, lo);
+    *reinterpret_cast<uint4*>(table + 16 * i) = make_uint4(v, v, v, v);
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  const uint32_t lane4 = (lane & (C - 1)) * 4;
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int g = 0; g < MT; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t part[NS][MT];                                  // independent MFMA chains, scaled after the loop
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const uint32_t wd[2] = {w[s].x, w[s].y};
+    uint32_t l[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      l[i] = *reinterpret_cast<const uint32_t*>(table + ((((wd[i >> 2] >> (8 * (i & 3))) & 0xFF) * (4 * C)) | lane4));
+    const uint4 b0 = make_uint4(l[0], l[1], l[2], l[3]), b1 = make_uint4(l[4], l[5], l[6], l[7]);
+#pragma unroll
+    for (int g = 0; g < MT; ++g) {
+      const int t = 16 * g + j;                          // this lane's token row for the A fragment
+      const int lg0 = 8 * s + 2 * c;
+      const int ph0 = (lg0 & ~15) | ((lg0 ^ t) & 15), ph1 = ((lg0 + 1) & ~15) | (((lg0 + 1) ^ t) & 15);
+      const uint4 x0 = *reinterpret_cast<const uint4*>(xs + t * ROWB + 16 * ph0);
+      const uint4 x1 = *reinterpret_cast<const uint4*>(xs + t * ROWB + 16 * ph1);
+      part[s][g] = Mfma<T>::mma(x1, b1, Mfma<T>::mma(x0, b0, f32x4_t{0.f, 0.f, 0.f, 0.f}));
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const float a = s < ns ? am[s] : 0.0f;
+#pragma unroll
+    for (int g = 0; g < MT; ++g)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[g][v] = fmaf(part[s][g][v], a, acc[g][v]);
+  }
+  // D[token 4c + v][row j] (+16 g)
+  const int orow = rb * 64 + 16 * wave + j;
+  if (orow >= N) return;
+#pragma unroll
+  for (int g = 0; g < MT; ++g)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int t = 16 * g + 4 * c + v;
+      if (t >= M) continue;
+      if (nsplit > 1) ws[((long long)split * M + t) * N + orow] = acc[g][v];
+      else out[(long long)t * ldc + orow] = Io<T>::from_f32(acc[g][v]);
+    }
+}
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? atoi(argv[1]) : 11008, K = argc > 2 ? atoi(argv[2]) : 4096, M = argc > 3 ? atoi(argv[3]) : 8;
+  const int COPIES = 14, BS = 64;
+  std::vector<uint8_t*> W(COPIES);
+  std::vector<float*> AM(COPIES);
+  for (int c = 0; c < COPIES; ++c) { CK(hipMalloc(&W[c], (size_t)N * K / 2)); CK(hipMalloc(&AM[c], (size_t)N * K / BS * 4)); }
+  uint16_t *X, *Y, *Y2; float *code, *ws;
+  CK(hipMalloc(&X, (size_t)M * K * 2)); CK(hipMalloc(&Y, (size_t)M * N * 2)); CK(hipMalloc(&Y2, (size_t)M * N * 2));
+  CK(hipMalloc(&code, 64)); CK(hipMalloc(&ws, (size_t)64 * M * N * 4));
+  std::vector<uint8_t> hw((size_t)N * K / 2);
+  std::vector<float> ha((size_t)N * K / BS), hc(16);
+  std::vector<uint16_t> hx((size_t)M * K);
+  {
+    uint32_t r = 7;
+    for (auto& v : hw) { r = r * 1664525u + 1013904223u; v = (uint8_t)(r >> 24); }
+    for (auto& v : ha) { r = r * 1664525u + 1013904223u; v = 0.01f + (r >> 8) / 16777216.0f * 0.05f; }
+    for (int c = 0; c < COPIES; ++c) { CK(hipMemcpy(W[c], hw.data(), hw.size(), hipMemcpyHostToDevice)); CK(hipMemcpy(AM[c], ha.data(), ha.size() * 4, hipMemcpyHostToDevice)); }
+    for (auto& v : hx) { r = r * 1664525u + 1013904223u; v = (uint16_t)(0x3c00 + (r >> 28)) ^ ((r >> 20) & 1 ? 0x8000 : 0); }
+    CK(hipMemcpy(X, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
+    for (int i = 0; i < 16; ++i) hc[i] = (i - 7.5f) / 8;
+    CK(hipMemcpy(code, hc.data(), 64, hipMemcpyHostToDevice));
+  }
+  const int MT = M <= 16 ? 1 : 2;
+  const int s = skinny_splits(M, K);
+  const int grid = ((N + SK_ROWS - 1) / SK_ROWS) * s;
+  printf("N=%d K=%d M=%d: %d splits, %d workgroups, weights %.1f MB\n", N, K, M, s, grid, N * (double)K / 2e6);
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  auto lib = [&](int i, uint16_t* y) {
+    SkStats st{AM[i % COPIES], nullptr, nullptr, nullptr, nullptr, __builtin_ctz(BS), 0};
+    if (MT == 1) hipLaunchKernelGGL((k_gemm_4bit_skinny<bf16_t, 1, 10, false, 0>), dim3(grid), dim3(SK_THREADS), 0, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, st, code, ws, (bf16_t*)y, N, s);
+    else hipLaunchKernelGGL((k_gemm_4bit_skinny<bf16_t, 2, 5, false, 0>), dim3(grid), dim3(SK_THREADS), 0, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, st, code, ws, (bf16_t*)y, N, s);
+    if (s > 1) hipLaunchKernelGGL((k_skinny_reduce<bf16_t>), dim3((unsigned)(((long long)M * N / 4 + 255) / 256 + 1)), dim3(256), 0, 0, ws, s, M, N, (bf16_t*)y, N);
+  };
+  auto ftc = [&](auto k1, auto k2, int C) {
+    return [=](int i, uint16_t* y) {
+      if (MT == 1) hipLaunchKernelGGL(k1, dim3(grid), dim3(256), 1024 * C + 16 * 20 * 128, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, AM[i % COPIES], code, ws, (bf16_t*)y, N, s);
+      else hipLaunchKernelGGL(k2, dim3(grid), dim3(256), 1024 * C + 32 * 10 * 128, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, AM[i % COPIES], code, ws, (bf16_t*)y, N, s);
+      if (s > 1) hipLaunchKernelGGL((k_skinny_reduce<bf16_t>), dim3((unsigned)(((long long)M * N / 4 + 255) / 256 + 1)), dim3(256), 0, 0, ws, s, M, N, (bf16_t*)y, N);
+    };
+  };
+  auto ft = ftc(k_ft<bf16_t, 1, 20, 32>, k_ft<bf16_t, 2, 10, 32>, 32);
+  auto ft8 = ftc(k_ft<bf16_t, 1, 20, 8>, k_ft<bf16_t, 2, 10, 8>, 8);
+  auto ft4 = ftc(k_ft<bf16_t, 1, 20, 4>, k_ft<bf16_t, 2, 10, 4>, 4);
+  {   // agreement: both against an fp64 product of (code * absmax) x X on 256 sampled outputs
+    ft8(0, Y2); CK(hipDeviceSynchronize());
+    std::vector<uint16_t> z1((size_t)M * N), z2((size_t)M * N);
+    CK(hipMemcpy(z1.data(), Y2, z1.size() * 2, hipMemcpyDeviceToHost));
+    ft4(0, Y2); CK(hipDeviceSynchronize());
+    CK(hipMemcpy(z2.data(), Y2, z2.size() * 2, hipMemcpyDeviceToHost));
+    lib(0, Y); ft(0, Y2); CK(hipDeviceSynchronize());
+    std::vector<uint16_t> y1((size_t)M * N), y2((size_t)M * N);
+    CK(hipMemcpy(y1.data(), Y, y1.size() * 2, hipMemcpyDeviceToHost)); CK(hipMemcpy(y2.data(), Y2, y2.size() * 2, hipMemcpyDeviceToHost));
+    auto bf = [](uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return (double)f; };
+    double e1m = 0, e2m = 0, refm = 0;
+    for (int q = 0; q < 256; ++q) {
+      const int t = q % M, n = (int)((q * 2654435761u) % N);
+      double ref = 0;
+      for (int k = 0; k < K; ++k) {
+        const uint8_t byte = hw[((size_t)n * K + k) / 2];
+        const int qq = (k & 1) ? (byte & 15) : (byte >> 4);
+        ref += bf(hx[(size_t)t * K + k]) * (double)hc[qq] * ha[((size_t)n * K + k) / 64];
+      }
+      e1m = std::max(e1m, fabs(bf(y1[(size_t)t * N + n]) - ref));
+      e2m = std::max(e2m, fabs(bf(y2[(size_t)t * N + n]) - ref));
+      refm = std::max(refm, fabs(ref));
+    }
+    printf("max |err| vs fp64: library %.4g  k_ft %.4g  (max |ref| %.4g); 8/4 copies bit-identical to 32: %s %s\n", e1m, e2m, refm,
+           memcmp(z1.data(), y2.data(), z1.size() * 2) ? "NO" : "yes", memcmp(z2.data(), y2.data(), z2.size() * 2) ? "NO" : "yes");
+  }
+  struct V { const char* name; std::function<void(int)> fn; std::vector<double> us; };
+  std::vector<V> vs;
+  vs.push_back({"library skinny + reduce", [&](int i) { lib(i, Y); }, {}});
+  vs.push_back({"library skinny main only", [&](int i) {
+                  SkStats st{AM[i % COPIES], nullptr, nullptr, nullptr, nullptr, __builtin_ctz(BS), 0};
+                  if (MT == 1) hipLaunchKernelGGL((k_gemm_4bit_skinny<bf16_t, 1, 10, false, 0>), dim3(grid), dim3(SK_THREADS), 0, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, st, code, ws, (bf16_t*)Y, N, s);
+                  else hipLaunchKernelGGL((k_gemm_4bit_skinny<bf16_t, 2, 5, false, 0>), dim3(grid), dim3(SK_THREADS), 0, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, st, code, ws, (bf16_t*)Y, N, s);
+                }, {}});
+  vs.push_back({"k_ft 32 copies + reduce", [&](int i) { ft(i, Y2); }, {}});
+  vs.push_back({"k_ft 8 copies + reduce", [&](int i) { ft8(i, Y2); }, {}});
+  vs.push_back({"k_ft 4 copies + reduce", [&](int i) { ft4(i, Y2); }, {}});
+  for (int i = 0; i < 50; ++i) for (auto& v : vs) v.fn(i);
+  CK(hipDeviceSynchronize());
+  for (int rep = 0; rep < 15; ++rep)
+    for (auto& v : vs) {
+      for (int i = 0; i < 14; ++i) v.fn(i);
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 28; ++i) v.fn(i);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1e3 / 28);
+    }
+  for (auto& v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    printf("%-28s median %7.2f us (back to back, incl. reduce)\n", v.name, v.us[v.us.size() / 2]);
+  }
+  return 0;
+}
