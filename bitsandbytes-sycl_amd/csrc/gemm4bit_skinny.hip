@@ -202,18 +202,34 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
   }
 }
 
-// out[t, n] = T(sum_s ws[s][t][n]), splits summed in order (fp32), one RNE cast; 4 outputs per thread
+// out[t, n] = T(sum_s ws[s][t][n]), splits summed in order (fp32), one RNE cast; 4 outputs per thread.
+// The partials were just written by other XCDs (read back through the MALL), so the loads of up to 8 splits
+// are issued together (indices clamped, unconditional) before any add: one round trip for the usual 4..7
+// splits instead of one per split.  Same additions in the same order as a sequential loop.
 template <typename T>
 __global__ void __launch_bounds__(256)
 k_skinny_reduce(const float* __restrict__ ws, int nsplit, int M, int N, T* __restrict__ out, int ldc) {
+  constexpr int BATCH = 8;
   const long long mn = (long long)M * N;
   const long long i0 = 4 * ((long long)blockIdx.x * 256 + threadIdx.x);
   if (i0 >= mn) return;
   if ((N & 3) == 0) {
-    float4 s = *reinterpret_cast<const float4*>(ws + i0);
-    for (int k = 1; k < nsplit; ++k) {
-      const float4 v = *reinterpret_cast<const float4*>(ws + k * mn + i0);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k0 = 0; k0 < nsplit; k0 += BATCH) {
+      float4 v[BATCH];
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b)
+        v[b] = *reinterpret_cast<const float4*>(ws + min(k0 + b, nsplit - 1) * mn + i0);
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b) {
+        const bool live = k0 + b < nsplit;
+        if (k0 + b == 0) {
+          s = v[0];
+        } else {
+          s.x = live ? s.x + v[b].x : s.x; s.y = live ? s.y + v[b].y : s.y;
+          s.z = live ? s.z + v[b].z : s.z; s.w = live ? s.w + v[b].w : s.w;
+        }
+      }
     }
     const long long t = i0 / N, n = i0 - t * N;
     T* dst = out + t * ldc + n;
