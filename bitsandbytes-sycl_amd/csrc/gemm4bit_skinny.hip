@@ -31,6 +31,11 @@ namespace bnb {
 #define LUTC_DEF 1
 #endif
 
+// timeline hooks for tools/fewtoken_lab.hip (no code in the library build)
+#ifndef SK_STAMP
+#define SK_STAMP(i)
+#endif
+
 constexpr int SK_THREADS = 256, SK_ROWS = 64, SK_LUTC = LUTC_DEF, SK_MAX_TOKENS = 32;
 
 
@@ -64,6 +69,7 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
   const int rowc = min(rb * SK_ROWS + 16 * wave + r, N - 1);
   const int kb0 = split * NB;                                  // first 128-k block of this split
   const int nb = min(NB, (K >> 7) - kb0);                      // >= 1 by construction
+  SK_STAMP(0);
 
   // (1a) table values and statistics first: their consumers must not wait on the weight loads below
   // (the VMEM counter retires in order)
@@ -127,6 +133,7 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
+  SK_STAMP(1);
   const float2* lutc = lut + (lane & (SK_LUTC - 1));
 
   // (3) per block, as its weights land: 16 table pairs (read one block ahead), one 16-row x 32-k A
@@ -180,6 +187,7 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[0][g][i] = (acc[0][g][i] + acc[1][g][i]) + (acc[2][g][i] + acc[3][g][i]);
 
+  SK_STAMP(2);
   // D[i]: weight row 4c + i of the wave's 16, token 16g + r -> 4 consecutive features per lane
   const int row0 = rb * SK_ROWS + 16 * wave + 4 * c;
 #pragma unroll

@@ -3,6 +3,16 @@
 // straight from a conflict-free bf16 pair table {T(code[hi]), T(code[lo])} (32 copies, GEMV layout) and scales
 // each 64-k step's MFMA sum by the lane's own absmax (D[token][row]: a lane holds one weight row).
 // 8 tokens x 11008 x 4096 by default (argv: N K M), 14 rotating weight copies, plain fp32 absmax.
+#include <hip/hip_runtime.h>
+// per-wave timeline of the library kernel: s_memrealtime (100 MHz) at start, after the post-fill barrier, after the
+// last MFMA; lane 0 of each wave, plain vector stores into a buffer of its own
+__device__ unsigned long long* g_stamps;
+__device__ __forceinline__ void sk_stamp(int i) {
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) g_stamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 3 + i] = t;
+}
+#define SK_STAMP(i) sk_stamp(i)
+
 #include "gemm4bit_skinny.hip"
 #include <algorithm>
 #include <cmath>
@@ -128,6 +138,204 @@ k_ft(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __res
     }
 }
 
+// Timing-only variant (W16): the lane's weights as one 16-B load per 128-k block (elements 32c..32c+31), the
+// four sub-steps using dwords 0..3, one absmax per 128-k block -- isolates the load shape from the block mixing.
+template <typename T, int MT, int NS2, int C = 32>
+__global__ void __launch_bounds__(256, 2)
+k_ft16(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
+       const float* __restrict__ absmax, const float* __restrict__ code, float* __restrict__ ws, T* __restrict__ out,
+       int ldc, int nsplit) {
+  constexpr int MP = 16 * MT;
+  constexpr int ROWB = NS2 * 256;
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  uint8_t* table = sm;
+  uint8_t* xs = sm + 256 * 4 * C;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rb = blockIdx.x / nsplit, split = blockIdx.x - rb * nsplit;
+  const int j = lane & 15, c = lane >> 4;
+  const int row = min(rb * 64 + 16 * wave + j, N - 1);
+  const int s0 = split * NS2;
+  const int ns = min(NS2, (K >> 7) - s0);
+  float dt[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dt[i] = code[i];
+  float am[NS2];
+#pragma unroll
+  for (int s = 0; s < NS2; ++s) am[s] = absmax[((long long)row * K + 128LL * (s0 + min(s, ns - 1))) >> 6];
+  constexpr int SLOTS = MP * NS2 * 16;
+  for (int p = wave; p * 64 < SLOTS; p += 4) {
+    const int i = p * 64 + lane;
+    const int t = i / (NS2 * 16), ph = i - t * (NS2 * 16);
+    const int lg = (ph & ~15) | ((ph ^ t) & 15);
+    const int step = lg >> 4;
+    if (step < ns) glds16(A + (long long)min(t, M - 1) * lda + 128LL * s0 + 8 * lg, xs + p * 1024);
+    else *reinterpret_cast<uint4*>(xs + 16 * i) = make_uint4(0, 0, 0, 0);
+  }
+  uintptr_t bp = (uintptr_t)B;
+  asm volatile("" : "+s"(bp)::"memory");
+  typedef const __attribute__((address_space(1))) u32x4_t* gv4_t;
+  uint4 w[NS2];
+  const gb_t wp = (gb_t)bp + (long long)row * ldb + 64LL * s0 + 16 * c;
+#pragma unroll
+  for (int s = 0; s < NS2; ++s) {
+    const u32x4_t v = __builtin_nontemporal_load((gv4_t)(wp + 64 * min(s, ns - 1)));
+    w[s] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+  for (int i = tid; i < 256 * C / 4; i += 256) {
+    const int e = i / (C / 4);
+    float hi = dt[0], lo = dt[0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) { hi = (e >> 4) == q ? dt[q] : hi; lo = (e & 15) == q ? dt[q] : lo; }
+    const uint32_t v = Pair<T>::make(hi, lo);
+    *reinterpret_cast<uint4*>(table + 16 * i) = make_uint4(v, v, v, v);
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS2) : "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  const uint32_t lane4 = (lane & (C - 1)) * 4;
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int g = 0; g < MT; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS2; ++s) {
+    const uint32_t wd[4] = {w[s].x, w[s].y, w[s].z, w[s].w};
+    f32x4_t part[MT];
+#pragma unroll
+    for (int g = 0; g < MT; ++g) part[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t l[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        l[i] = *reinterpret_cast<const uint32_t*>(table + ((((wd[q] >> (8 * i)) & 0xFF) * (4 * C)) | lane4));
+      const uint4 b = make_uint4(l[0], l[1], l[2], l[3]);
+#pragma unroll
+      for (int g = 0; g < MT; ++g) {
+        const int t = 16 * g + j;
+        const int lg = 16 * s + 4 * c + q;
+        const int ph = (lg & ~15) | ((lg ^ t) & 15);
+        const uint4 x = *reinterpret_cast<const uint4*>(xs + t * ROWB + 16 * ph);
+        part[g] = Mfma<T>::mma(x, b, part[g]);
+      }
+    }
+    const float a = s < ns ? am[s] : 0.0f;
+#pragma unroll
+    for (int g = 0; g < MT; ++g)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[g][v] = fmaf(part[g][v], a, acc[g][v]);
+  }
+  const int orow = rb * 64 + 16 * wave + j;
+  if (orow >= N) return;
+#pragma unroll
+  for (int g = 0; g < MT; ++g)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int t = 16 * g + 4 * c + v;
+      if (t >= M) continue;
+      if (nsplit > 1) ws[((long long)split * M + t) * N + orow] = acc[g][v];
+      else out[(long long)t * ldc + orow] = Io<T>::from_f32(acc[g][v]);
+    }
+}
+
+template <typename T, int MT, int NS2, int C = 32>
+__global__ void __launch_bounds__(256, 2)
+k_ft16r(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
+       const float* __restrict__ absmax, const float* __restrict__ code, float* __restrict__ ws, T* __restrict__ out,
+       int ldc, int nsplit) {
+  constexpr int MP = 16 * MT;
+  constexpr int ROWB = NS2 * 256;
+  extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+  uint8_t* table = sm;
+  uint8_t* xs = sm + 256 * 4 * C;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rb = blockIdx.x / nsplit, split = blockIdx.x - rb * nsplit;
+  const int j = lane & 15, c = lane >> 4;
+  const int row = min(rb * 64 + 16 * wave + j, N - 1);
+  const int s0 = split * NS2;
+  const int ns = min(NS2, (K >> 7) - s0);
+  float dt[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dt[i] = code[i];
+  float am[NS2];
+#pragma unroll
+  for (int s = 0; s < NS2; ++s) am[s] = absmax[((long long)row * K + 128LL * (s0 + min(s, ns - 1))) >> 6];
+  const int T4 = 4 * ((M + 3) / 4);                    // staged token rows (the rest read the zero row)
+  const int SLOTS = T4 * NS2 * 16;
+  for (int i = tid; i < NS2 * 16; i += 256) *reinterpret_cast<uint4*>(xs + MP * ROWB + 16 * i) = make_uint4(0, 0, 0, 0);
+  for (int p = wave; p * 64 < SLOTS; p += 4) {
+    const int i = p * 64 + lane;
+    const int t = i / (NS2 * 16), ph = i - t * (NS2 * 16);
+    const int lg = (ph & ~15) | ((ph ^ t) & 15);
+    const int step = lg >> 4;
+    if (step < ns) glds16(A + (long long)min(t, M - 1) * lda + 128LL * s0 + 8 * lg, xs + p * 1024);
+    else *reinterpret_cast<uint4*>(xs + 16 * i) = make_uint4(0, 0, 0, 0);
+  }
+  uintptr_t bp = (uintptr_t)B;
+  asm volatile("" : "+s"(bp)::"memory");
+  typedef const __attribute__((address_space(1))) u32x4_t* gv4_t;
+  uint4 w[NS2];
+  const gb_t wp = (gb_t)bp + (long long)row * ldb + 64LL * s0 + 16 * c;
+#pragma unroll
+  for (int s = 0; s < NS2; ++s) {
+    const u32x4_t v = __builtin_nontemporal_load((gv4_t)(wp + 64 * min(s, ns - 1)));
+    w[s] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+  for (int i = tid; i < 256 * C / 4; i += 256) {
+    const int e = i / (C / 4);
+    float hi = dt[0], lo = dt[0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) { hi = (e >> 4) == q ? dt[q] : hi; lo = (e & 15) == q ? dt[q] : lo; }
+    const uint32_t v = Pair<T>::make(hi, lo);
+    *reinterpret_cast<uint4*>(table + 16 * i) = make_uint4(v, v, v, v);
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS2) : "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  const uint32_t lane4 = (lane & (C - 1)) * 4;
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int g = 0; g < MT; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS2; ++s) {
+    const uint32_t wd[4] = {w[s].x, w[s].y, w[s].z, w[s].w};
+    f32x4_t part[MT];
+#pragma unroll
+    for (int g = 0; g < MT; ++g) part[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t l[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        l[i] = *reinterpret_cast<const uint32_t*>(table + ((((wd[q] >> (8 * i)) & 0xFF) * (4 * C)) | lane4));
+      const uint4 b = make_uint4(l[0], l[1], l[2], l[3]);
+#pragma unroll
+      for (int g = 0; g < MT; ++g) {
+        const int t = 16 * g + j;
+        const int lg = 16 * s + 4 * c + q;
+        const int ph = (lg & ~15) | ((lg ^ t) & 15);
+        const uint4 x = *reinterpret_cast<const uint4*>(xs + (t < T4 ? t : MP) * ROWB + 16 * ph);
+        part[g] = Mfma<T>::mma(x, b, part[g]);
+      }
+    }
+    const float a = s < ns ? am[s] : 0.0f;
+#pragma unroll
+    for (int g = 0; g < MT; ++g)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[g][v] = fmaf(part[g][v], a, acc[g][v]);
+  }
+  const int orow = rb * 64 + 16 * wave + j;
+  if (orow >= N) return;
+#pragma unroll
+  for (int g = 0; g < MT; ++g)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int t = 16 * g + 4 * c + v;
+      if (t >= M) continue;
+      if (nsplit > 1) ws[((long long)split * M + t) * N + orow] = acc[g][v];
+      else out[(long long)t * ldc + orow] = Io<T>::from_f32(acc[g][v]);
+    }
+}
+
 int main(int argc, char** argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 11008, K = argc > 2 ? atoi(argv[2]) : 4096, M = argc > 3 ? atoi(argv[3]) : 8;
   const int COPIES = 14, BS = 64;
@@ -153,6 +361,10 @@ int main(int argc, char** argv) {
   const int MT = M <= 16 ? 1 : 2;
   const int s = skinny_splits(M, K);
   const int grid = ((N + SK_ROWS - 1) / SK_ROWS) * s;
+  // the library kernel stamps every launch (SK_STAMP): its buffer is set before the first launch
+  unsigned long long* st; CK(hipMalloc(&st, (size_t)grid * 4 * 3 * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
+
   printf("N=%d K=%d M=%d: %d splits, %d workgroups, weights %.1f MB\n", N, K, M, s, grid, N * (double)K / 2e6);
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto lib = [&](int i, uint16_t* y) {
@@ -171,6 +383,12 @@ int main(int argc, char** argv) {
   auto ft = ftc(k_ft<bf16_t, 1, 20, 32>, k_ft<bf16_t, 2, 10, 32>, 32);
   auto ft8 = ftc(k_ft<bf16_t, 1, 20, 8>, k_ft<bf16_t, 2, 10, 8>, 8);
   auto ft4 = ftc(k_ft<bf16_t, 1, 20, 4>, k_ft<bf16_t, 2, 10, 4>, 4);
+  auto ft16 = ftc(k_ft16<bf16_t, 1, 10, 8>, k_ft16<bf16_t, 2, 5, 8>, 8);
+  auto ft16r = [&](int i, uint16_t* y) {   // + one zero row of NS2 * 256 B
+    if (MT == 1) hipLaunchKernelGGL((k_ft16r<bf16_t, 1, 10, 8>), dim3(grid), dim3(256), 1024 * 8 + 17 * 10 * 256, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, AM[i % COPIES], code, ws, (bf16_t*)y, N, s);
+    else hipLaunchKernelGGL((k_ft16r<bf16_t, 2, 5, 8>), dim3(grid), dim3(256), 1024 * 8 + 33 * 5 * 256, 0, N, M, K, (const bf16_t*)X, K, W[i % COPIES], K / 2, AM[i % COPIES], code, ws, (bf16_t*)y, N, s);
+    if (s > 1) hipLaunchKernelGGL((k_skinny_reduce<bf16_t>), dim3((unsigned)(((long long)M * N / 4 + 255) / 256 + 1)), dim3(256), 0, 0, ws, s, M, N, (bf16_t*)y, N);
+  };
   {   // agreement: both against an fp64 product of (code * absmax) x X on 256 sampled outputs
     ft8(0, Y2); CK(hipDeviceSynchronize());
     std::vector<uint16_t> z1((size_t)M * N), z2((size_t)M * N);
@@ -197,6 +415,26 @@ int main(int argc, char** argv) {
     printf("max |err| vs fp64: library %.4g  k_ft %.4g  (max |ref| %.4g); 8/4 copies bit-identical to 32: %s %s\n", e1m, e2m, refm,
            memcmp(z1.data(), y2.data(), z1.size() * 2) ? "NO" : "yes", memcmp(z2.data(), y2.data(), z2.size() * 2) ? "NO" : "yes");
   }
+  {   // timeline (one launch after warm-up, weights copy 3)
+    for (int i = 0; i < 20; ++i) lib(i, Y);
+    lib(3, Y); CK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h((size_t)grid * 12);
+    CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull, tend = 0;
+    for (size_t w = 0; w < h.size() / 3; ++w) { t0 = std::min(t0, h[3 * w]); tend = std::max(tend, h[3 * w + 2]); }
+    std::vector<double> start, fill, comp, end;
+    for (size_t w = 0; w < h.size() / 3; ++w) {
+      start.push_back((h[3 * w] - t0) * 0.01); fill.push_back((h[3 * w + 1] - h[3 * w]) * 0.01);
+      comp.push_back((h[3 * w + 2] - h[3 * w + 1]) * 0.01); end.push_back((h[3 * w + 2] - t0) * 0.01);
+    }
+    auto pr = [](const char* n, std::vector<double> v) {
+      std::sort(v.begin(), v.end());
+      printf("  %-34s p5 %6.2f  p50 %6.2f  p95 %6.2f  max %6.2f us\n", n, v[v.size() / 20], v[v.size() / 2], v[v.size() * 19 / 20], v.back());
+    };
+    printf("timeline (main kernel, span %.2f us):\n", (tend - t0) * 0.01);
+    pr("wave start", start); pr("start -> post-fill barrier", fill); pr("barrier -> last MFMA", comp); pr("wave end", end);
+
+  }
   struct V { const char* name; std::function<void(int)> fn; std::vector<double> us; };
   std::vector<V> vs;
   vs.push_back({"library skinny + reduce", [&](int i) { lib(i, Y); }, {}});
@@ -208,6 +446,8 @@ int main(int argc, char** argv) {
   vs.push_back({"k_ft 32 copies + reduce", [&](int i) { ft(i, Y2); }, {}});
   vs.push_back({"k_ft 8 copies + reduce", [&](int i) { ft8(i, Y2); }, {}});
   vs.push_back({"k_ft 4 copies + reduce", [&](int i) { ft4(i, Y2); }, {}});
+  vs.push_back({"k_ft16 (16-B loads, timing only)", [&](int i) { ft16(i, Y2); }, {}});
+  vs.push_back({"k_ft16r (+ real token rows only)", [&](int i) { ft16r(i, Y2); }, {}});
   for (int i = 0; i < 50; ++i) for (auto& v : vs) v.fn(i);
   CK(hipDeviceSynchronize());
   for (int rep = 0; rep < 15; ++rep)
