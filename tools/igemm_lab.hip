@@ -374,6 +374,134 @@ k_igemm_w4(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __re
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 }
+
+// v_mfma_i32_32x32x32_i8 variant of the library kernel (ROW A, ROW B, fused fp16 dequant): per wave 128 x 64 as
+// 4 x 2 tiles of 32x32, k32 per MFMA (4 sub-steps per 128-B k-tile) -> 6 fragment reads per 8 MFMAs (the 16x16x64
+// form reads 12 per 32).  Lane l holds 16 k of row l & 31, k-chunk l >> 5 (A and B alike); the (row >> 1) & 7 swizzle
+// makes the 32-row fragment reads conflict-free.  D[r]: row 8 (r >> 2) + 4 (l >> 5) + (r & 3), col l & 31.
+typedef __attribute__((ext_vector_type(16))) int i32x16_t;
+__device__ __forceinline__ int swzh(int r, int s) { return r * 128 + ((s ^ ((r >> 1) & 7)) << 4); }
+
+template <int FL>
+__global__ void __launch_bounds__(J_THREADS, 1)
+k_igemm_32(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restrict__ B, fp16_t* __restrict__ out,
+           long long lda, long long ldb, long long ldc, const float* __restrict__ rowStats,
+           const float* __restrict__ colStats, const fp16_t* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[J_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (N + J_BN - 1) / J_BN, tilesM = (M + J_BM - 1) / J_BM;
+  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  constexpr int GROUP = 4;
+  const int group_span = GROUP * tilesN;
+  const int first_m = (wg / group_span) * GROUP;
+  const int gsize = min(tilesM - first_m, GROUP);
+  const int tm = first_m + (wg % group_span) % gsize;
+  const int tn = (wg % group_span) / gsize;
+  const int m0 = tm * J_BM, n0 = tn * J_BN;
+  long long arow[4], brow[4];
+  int kslot[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wave + i) + (lane >> 3);
+    arow[i] = min(m0 + row, M - 1);
+    brow[i] = min(n0 + row, N - 1);
+    kslot[i] = 16 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  auto dma = [&](int kt, int buf) {
+    const long long k0 = (long long)kt * J_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(A + arow[i] * lda + k0 + kslot[i], smem + buf * J_TILE + (4 * wave + i) * 1024);
+      glds16(B + brow[i] * ldb + k0 + kslot[i], smem + 2 * J_TILE + buf * J_TILE + (4 * wave + i) * 1024);
+    }
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  i32x16_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+  // fragments of sub-steps (ks, ks + 1) in one set: a[2][4], b[2][2]
+  auto frag = [&](int buf, int kp, uint4 (&a)[2][4], uint4 (&b)[2][2]) {
+    const uint8_t* as = smem + buf * J_TILE;
+    const uint8_t* bs = smem + 2 * J_TILE + buf * J_TILE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int slot = 2 * (2 * kp + h) + (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[h][j] = *reinterpret_cast<const uint4*>(bs + swzh(64 * wn + 32 * j + (lane & 31), slot));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[h][i] = *reinterpret_cast<const uint4*>(as + swzh(128 * wm + 32 * i + (lane & 31), slot));
+    }
+  };
+  auto mma = [&](const uint4 (&a)[2][4], const uint4 (&b)[2][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(i32x4_t, a[h][i]), __builtin_bit_cast(i32x4_t, b[h][j]),
+                                                            acc[i][j], 0, 0, 0);
+  };
+  const int nk = K / J_BK;
+  dma(0, 0);
+  if (nk > 1) {
+    dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    wait_vmcnt0();
+  }
+  __syncthreads();
+  uint4 fa[2][2][4], fb[2][2][2];
+  frag(0, 0, fa[0], fb[0]);
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    frag(s, 1, fa[1], fb[1]);
+    mma(fa[0], fb[0]);
+    wait_vmcnt0();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) dma(t + 2, s);
+    if (t + 1 < nk) frag(s ^ 1, 0, fa[0], fb[0]);
+    mma(fa[1], fb[1]);
+  }
+  __syncthreads();
+  const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;
+  uint8_t* ep = smem + wave * (128 * J_EPI_STRIDE);
+  float cs[2], bv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = min(gcol0 + 32 * j + (lane & 31), N - 1);
+    cs[j] = colStats[col];
+    bv[j] = bias ? (float)bias[col] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * i + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+      const float rs = rowStats[min(grow0 + row, M - 1)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<fp16_t*>(ep + row * J_EPI_STRIDE + 2 * (32 * j + (lane & 31))) = mm_dequant_value(acc[i][j][r], rs, cs[j], bv[j]);
+    }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int id = lane + 64 * it;
+    const int row = id >> 3, c8 = id & 7;
+    const int grow = grow0 + row, gcol = gcol0 + 8 * c8;
+    if (grow >= M) continue;
+    const uint2 lo = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8);
+    const uint2 hi = *reinterpret_cast<const uint2*>(ep + row * J_EPI_STRIDE + 16 * c8 + 8);
+    fp16_t* dst = out + (long long)grow * ldc + gcol;
+    if (gcol + 8 <= N) *reinterpret_cast<uint4*>(dst) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
 }  // namespace bnb
 using namespace bnb;
 
@@ -434,6 +562,7 @@ int main(int argc, char** argv) {
   vs.push_back({"cross-barrier", v3(k_igemm_xb<0>), {}});
   auto w4 = [=]() { hipLaunchKernelGGL(k_igemm_w4, dim3(tiles), dim3(256), 0, 0, M, N, K, (const int8_t*)A, (const int8_t*)B, C1, (long long)K, (long long)K, (long long)N, (const float*)rs, (const float*)cs, (const fp16_t*)nullptr); };
   vs.push_back({"one wave per SIMD", w4, {}});
+  vs.push_back({"32x32x32 MFMA", v3(k_igemm_32<0>), {}});
   for (size_t v = 1; v < vs.size(); ++v) { vs[v].fn(); CK(hipDeviceSynchronize()); printf("%s", vs[v].name); check(); }
   for (int rep = 0; rep < 12; ++rep)
     for (auto& v : vs) {
