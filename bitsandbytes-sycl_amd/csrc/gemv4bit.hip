@@ -17,6 +17,7 @@
 // (byte -> {code[hi], code[lo]}), and reduces the R partial sums across the wave at the end.
 #include "common.hpp"
 #include "gemm_common.hpp"
+#include "gemv_common.hpp"
 
 namespace bnb {
 
@@ -125,40 +126,6 @@ k_gemv_4bit(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B
 //      consumed as soon as its load returns.
 // NESTED fuses the compressed-statistics decode (functional.py:1982-1984):
 //   absmax[j] = code2[q8[j]] * absmax2[j >> log2(bs2)] + offset, fp32, the dequantize_blockwise order.
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
-typedef const __attribute__((address_space(1))) uint8_t* gbyte_p;
-typedef const __attribute__((address_space(1))) u32x4_t* gvec_p;
-
-template <typename T> struct Dot2;
-template <> struct Dot2<bf16_t> {
-  __device__ static __forceinline__ float dot(uint32_t a, uint32_t b, float c) {
-    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
-  }
-  __device__ static __forceinline__ uint32_t pair(float lo, float hi) { return pack_bf16x2(lo, hi); }
-};
-template <> struct Dot2<fp16_t> {
-  __device__ static __forceinline__ float dot(uint32_t a, uint32_t b, float c) {
-    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, a), __builtin_bit_cast(f16x2_t, b), c, false);
-  }
-  __device__ static __forceinline__ uint32_t pair(float lo, float hi) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, (fp16_t)lo) | ((uint32_t)__builtin_bit_cast(uint16_t, (fp16_t)hi) << 16);
-  }
-};
-
-constexpr int GV_THREADS = 256;
-constexpr int GV_TABLE_BYTES = 256 * 128;    // 32 bank-private copies of the 256-entry pair table
-constexpr int GV_MAX_K = 16384;              // table + K/2 pairs of T within 64 KiB
-
-struct GemvStats {
-  const float* absmax;      // plain: fp32 per block
-  const uint8_t* q8;        // nested: 8-bit codes per block
-  const float* code2;       //         256-entry dynamic map
-  const float* absmax2;     //         fp32 per group of bs2 blocks
-  const float* offset;      //         scalar (device)
-  int bs_shift, bs2_shift;
-};
-
 template <typename T, int R, int U, bool NESTED>
 __global__ void __launch_bounds__(GV_THREADS)
 k_gemv_4bit_dot(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,

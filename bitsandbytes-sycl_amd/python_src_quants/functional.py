@@ -731,6 +731,9 @@ GEMM_4BIT_FEW_TOKENS = 32
 # 11008 x 4096 at 64 / 128 / 256 rows 53.8 / 58.8 / 67.5 vs 45.1 / 50.6 / 65.1; 4096 x 4096 27.0 / 31.8 / 35.0 vs
 # 29.5 / 36.0 / 34.0; 4096 x 11008 36.3 / 38.8 / 48.9 vs 52.7 / 71.2 / 64.4).
 GEMM_4BIT_WIDE_MAX_ROWS = 256
+# 2..GEMM_4BIT_GEMV_TOKENS activation rows run the multi-row GEMV (gemv4bit_tok.hip: every weight byte looked up
+# once and dotted with each row, whole K per workgroup, one launch, rows bit-identical to gemv_4bit on each row).
+GEMM_4BIT_GEMV_TOKENS = 4
 
 _DEQ_WS: dict = {}
 _DEQ_META: dict = {}
@@ -746,6 +749,38 @@ def _dequant_workspace(device, dtype, numel: int) -> Tensor:
         _DEQ_WS[key] = ws
         _DEQ_META.pop(key, None)
     return ws[:numel]
+
+
+def _gemm_4bit_tokens(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor],
+                      events: Optional[list]) -> bool:
+    """2..GEMM_4BIT_GEMV_TOKENS rows through cgemm_4bit_inference_tokens_* (one launch; compressed statistics
+    decoded in the kernel).  False when the entry point declines the shape (nothing launched)."""
+    N, K = state.shape[0], state.shape[1]
+    rows = A2.shape[0]
+    nested = absmax is None and _nested_stats_in_kernel_ok(state)
+    if nested:
+        s2 = state.state2
+        stats = [None, state.absmax, s2.code, s2.absmax, _offset_on(state, A2.device)]
+        bs2 = s2.blocksize
+    else:
+        stats = [absmax if absmax is not None else _absmax_fp32(state), None, None, None, None]
+        bs2 = 0
+    prev_device = pre_call(A2.device)
+    is_on_gpu([A2, Bc, out, state.code] + [t for t in stats if t is not None])
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if events is not None else None
+    if ev:
+        ev[0].record()
+    fn = lib.cgemm_4bit_inference_tokens_bf16 if A2.dtype == torch.bfloat16 else lib.cgemm_4bit_inference_tokens_fp16
+    rc = fn(ct.c_int32(N), ct.c_int32(rows), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(Bc),
+            ct.c_int32((K + 1) // 2), *[get_ptr(t) for t in stats], get_ptr(state.code), get_ptr(out), ct.c_int32(N),
+            ct.c_int32(state.blocksize), ct.c_int32(bs2))
+    post_call(prev_device)
+    if rc == 2:
+        raise RuntimeError(f"bitsandbytes HIP kernel error: {lib.cget_last_error_message().decode()}")
+    if rc == 0 and ev:
+        ev[1].record()
+        events.append(("gemm", ev[0], ev[1]))
+    return rc == 0
 
 
 def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = None,
@@ -772,6 +807,8 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
+    if not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events):
+        return out.view(*A.shape[:-1], N)
     if (absmax is None and not library and rows <= GEMM_4BIT_FEW_TOKENS and _nested_stats_in_kernel_ok(state)):
         # few tokens, compressed statistics: one launch of the weight-streaming kernel that decodes the
         # nested absmax in-kernel (no separate decode launch)

@@ -124,6 +124,19 @@ int cgemm_4bit_inference_nested_ws_fp16(int m, int n, int k, bnb_fp16* A, unsign
                                         float* code2, float* absmax2, float* offset, float* datatype, bnb_fp16* out,
                                         int lda, int ldb, int ldc, int blocksize, int blocksize2, float* workspace,
                                         long long workspace_bytes);
+/* [additive] 4-bit weight x 2..4 activation rows in one launch (gemv4bit_tok.hip; replaces the M > 1 pair
+ * dequantize_4bit + F.linear, ref:autograd/_functions.py:491-507, for batched decode): out[t * ldc + r], t < ntok.
+ * Statistics plain (absmax fp32, absmax_q = NULL) or compressed (absmax = NULL; absmax_q, code2, absmax2, offset,
+ * blocksize2) decoded in the kernel.  Each row t is bit-identical to cgemm_4bit_inference_naive_* on row t.
+ * Returns 0 when launched, 1 when the shape / alignment does not fit (nothing launched), 2 when the launch failed. */
+int cgemm_4bit_inference_tokens_bf16(int m, int ntok, int k, bnb_bf16* A, int lda, unsigned char* B, int ldb,
+                                     float* absmax, unsigned char* absmax_q, float* code2, float* absmax2,
+                                     float* offset, float* datatype, bnb_bf16* out, int ldc, int blocksize,
+                                     int blocksize2);
+int cgemm_4bit_inference_tokens_fp16(int m, int ntok, int k, bnb_fp16* A, int lda, unsigned char* B, int ldb,
+                                     float* absmax, unsigned char* absmax_q, float* code2, float* absmax2,
+                                     float* offset, float* datatype, bnb_fp16* out, int ldc, int blocksize,
+                                     int blocksize2);
 int cgemm_4bit_inference_nested_ws_bf16(int m, int n, int k, bnb_bf16* A, unsigned char* B, unsigned char* absmax_q,
                                         float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
                                         int lda, int ldb, int ldc, int blocksize, int blocksize2, float* workspace,

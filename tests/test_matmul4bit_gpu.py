@@ -362,12 +362,15 @@ def test_gemm_4bit_few_tokens_vs_oracle(dev, dtype, nested, mnk):
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
     frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
     assert frac == 0.0, err
-    # the tile kernels (forced) agree up to fp32 summation order
+    # the tile kernels (forced; the multi-row GEMV for 2..4 rows switched off) agree up to fp32 summation order
     F.lib.cgemm_4bit_set_tile(128)
+    saved = F.GEMM_4BIT_GEMV_TOKENS
+    F.GEMM_4BIT_GEMV_TOKENS = 1
     try:
         Yt = F.gemm_4bit(X, q, st, absmax=F._absmax_fp32(st))
     finally:
         F.lib.cgemm_4bit_set_tile(0)
+        F.GEMM_4BIT_GEMV_TOKENS = saved
     rms = Yt.float().pow(2).mean().sqrt().item()
     assert (Y.float() - Yt.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Yt.float().abs().max().item()
 
@@ -500,3 +503,72 @@ def test_gemv_plan_cache_follows_state_changes(dev, nested):
     assert yh.dtype == torch.float16 and torch.allclose(yh.float(), y1.float(), rtol=2e-2, atol=2e-2)
     out = torch.empty(1, N, device=dev, dtype=torch.bfloat16)
     assert F.gemv_4bit(x, q.t(), state=st, out=out) is out and torch.equal(out, y1)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("rows", [2, 3, 4])
+@pytest.mark.parametrize("shape", [(11008, 4096), (4096, 11008), (4096, 4096), (1001, 2048), (63, 128), (28672, 1024),
+                                   (3584, 8192), (40000, 4096)])
+def test_gemm_4bit_multirow_gemv_matches_gemv(dev, dtype, nested, rows, shape):
+    """2..4 activation rows run the multi-row GEMV (gemv4bit_tok.hip): every row of the result is bit-identical to
+    gemv_4bit on that row alone (same lookups, chains and wave reduction), plain and compressed statistics."""
+    F = _F()
+    N, K = shape
+    torch.manual_seed(N + K + rows)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(rows, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    Y = F.gemm_4bit(X, q, st)
+    assert Y.shape == (rows, N)
+    for t in range(rows):
+        y = F.gemv_4bit(X[t:t + 1], q.t(), state=st)
+        assert torch.equal(Y[t], y.reshape(-1)), f"row {t} differs from gemv_4bit"
+
+
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("qt,bs", [("nf4", 64), ("fp4", 64), ("nf4", 128), ("fp4", 256)])
+@pytest.mark.parametrize("mnk", [(2, 11008, 4096), (3, 1001, 2048), (4, 4099, 4096), (2, 1, 256)])
+def test_gemm_4bit_multirow_gemv_vs_oracle(dev, nested, qt, bs, mnk):
+    """The multi-row GEMV against the fp64 oracle of dequantize_4bit + matmul: FP4, blocksizes 64..256, ragged
+    out_features, one-row weights -- the GEMV tolerance (codes in T, fp32 products)."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M * 13 + N + bs)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
+    Y = F.gemm_4bit(X, q, st)
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, bs,
+                                    st.code.cpu().numpy(), "bf16")
+    frac, err = _close(Y.float().cpu().numpy(), exp, 2e-2, 2e-2)
+    assert frac == 0.0, err
+
+
+def test_gemm_4bit_multirow_gemv_entry_declines(dev):
+    """The multi-row entry point launches nothing (returns 1) for 1 or 5 rows; gemm_4bit then
+    takes the few-token kernel, which agrees with the multi-row GEMV up to summation order."""
+    F = _F()
+    N, K = 512, 1024
+    torch.manual_seed(77)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=False)
+    for M in (1, 5):
+        X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        rc = F.lib.cgemm_4bit_inference_tokens_bf16(
+            ct.c_int32(N), ct.c_int32(M), ct.c_int32(K), F.get_ptr(X), ct.c_int32(K), F.get_ptr(q), ct.c_int32(K // 2),
+            F.get_ptr(st.absmax), None, None, None, None, F.get_ptr(st.code), F.get_ptr(out), ct.c_int32(N),
+            ct.c_int32(64), ct.c_int32(0))
+        assert rc == 1
+    X = torch.randn(4, K, device=dev, dtype=torch.bfloat16)
+    Yg = F.gemm_4bit(X, q, st)
+    saved = F.GEMM_4BIT_GEMV_TOKENS
+    F.GEMM_4BIT_GEMV_TOKENS = 1
+    try:
+        Ys = F.gemm_4bit(X, q, st)
+    finally:
+        F.GEMM_4BIT_GEMV_TOKENS = saved
+    rms = Ys.float().pow(2).mean().sqrt().item()
+    assert (Yg.float() - Ys.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Ys.float().abs().max().item()
