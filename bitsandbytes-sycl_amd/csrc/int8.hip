@@ -292,6 +292,9 @@ k_double_rowcol_quant_wide(const fp16_t* __restrict__ A, const float* __restrict
 // -50000 the callers pre-fill when a row has no finite |a|), CA = rint(a * (127 / rowStats)).
 constexpr int RQ_MAX_VEC = 32;   // 16-B vectors per lane: K <= 16384
 
+// NV = 16-B vectors per lane (the smallest instance that holds the row: registers decide how many rows a CU keeps in
+// flight -- 32 vectors cost 171 VGPRs, two waves per SIMD)
+template <int NV>
 __global__ void __launch_bounds__(256)
 k_row_quant(const fp16_t* __restrict__ A, float* __restrict__ rowStats, int8_t* __restrict__ out, int rows, int cols) {
   const int lane = threadIdx.x & 63;
@@ -299,15 +302,15 @@ k_row_quant(const fp16_t* __restrict__ A, float* __restrict__ rowStats, int8_t* 
   if (row >= rows) return;
   const int nvec = cols >> 3;
   const uint4* src = reinterpret_cast<const uint4*>(A + (long long)row * cols);
-  uint4 v[RQ_MAX_VEC];
+  uint4 v[NV];
 #pragma unroll
-  for (int i = 0; i < RQ_MAX_VEC; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     if (c < nvec) v[i] = src[c];
   }
   float m = -3.402823466e+38f;
 #pragma unroll
-  for (int i = 0; i < RQ_MAX_VEC; ++i) {
+  for (int i = 0; i < NV; ++i) {
     if (lane + 64 * i < nvec) {
       const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
@@ -320,7 +323,7 @@ k_row_quant(const fp16_t* __restrict__ A, float* __restrict__ rowStats, int8_t* 
   const float rsc = __fdiv_rn(127.0f, m);
   uint2* dst = reinterpret_cast<uint2*>(out + (long long)row * cols);
 #pragma unroll
-  for (int i = 0; i < RQ_MAX_VEC; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     if (c < nvec) {
       const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
@@ -670,8 +673,18 @@ void cget_col_row_stats(fp16_t* A, float* rowStats, float* colStats, int* nnz_co
 int cint8_row_quant_fp16(fp16_t* A, float* rowStats, char* out_row, int rows, int cols) {
   if (rows <= 0 || cols <= 0) return 0;
   if (cols % 8 || cols > 64 * 8 * RQ_MAX_VEC || ((uintptr_t)A & 15) || ((uintptr_t)out_row & 7)) return 1;
-  hipLaunchKernelGGL(k_row_quant, dim3((rows + 3) / 4), dim3(256), 0, current_stream(), A, rowStats, (int8_t*)out_row,
-                     rows, cols);
+  const int per_lane = (cols / 8 + 63) / 64;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((rows + 3) / 4), dim3(256), 0, current_stream(), A, rowStats, (int8_t*)out_row, rows,
+                       cols);
+  };
+  if (per_lane <= 4) go(k_row_quant<4>);
+  else if (per_lane <= 8) go(k_row_quant<8>);
+  else if (per_lane <= 12) go(k_row_quant<12>);
+  else if (per_lane <= 16) go(k_row_quant<16>);
+  else if (per_lane <= 22) go(k_row_quant<22>);   // K = 11008: 22 vectors, 4 waves per SIMD
+  else if (per_lane <= 24) go(k_row_quant<24>);
+  else go(k_row_quant<RQ_MAX_VEC>);
   BNB_LAUNCH_CHECK("int8_row_quant");
   return 0;
 }
