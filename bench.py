@@ -46,6 +46,30 @@ def _events():
     return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
+# Per-stage events (dequantise / GEMM split, the roofline's kernel time) are recorded on every STAGE_EVERY-th timed
+# step only: an event record between two kernels costs the stream ~3-4 us on this stack, so five per step cost
+# ~18 us of a 250 us step (tools/step_overhead.py, profiles/lab/r02_step_overhead.txt).
+STAGE_EVERY = 10
+
+
+class StepClock:
+    """Step boundaries of the timed region as one chain of HIP events on the launching stream: one record
+    before the first step and one after each (K + 1 in all), so step i lasts ev[i] -> ev[i+1] and the
+    median over the K steps comes without a second event per step."""
+
+    def __init__(self, steps):
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        self.n = 0
+
+    def mark(self):
+        self.ev[self.n].record()
+        self.n += 1
+
+    def median_ms(self):
+        import statistics
+        return statistics.median(a.elapsed_time(b) for a, b in zip(self.ev[:self.n - 1], self.ev[1:self.n]))
+
+
 def _time_loop(fn, iters, warmup=3):
     for _ in range(warmup):
         fn()
@@ -112,19 +136,13 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
     del Wt
     lin = ColumnShardedLinear8bitLt(CB, SCB, world, rank)
     del CB
-    ev = []
+    clock = StepClock(steps)
 
-    def step(record=False):
-        if record:
-            s0, e0 = _events()
-            s0.record()
+    def step():
         if world > 1:
             lin.forward(A, assemble=True, chunks=chunks)
         else:
             lin.forward_local(A)
-        if record:
-            e0.record()
-            ev.append((s0, e0))
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -132,8 +150,10 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    clock.mark()
     for _ in range(steps):
-        step(record=True)
+        step()
+        clock.mark()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -145,8 +165,7 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
         elapsed = t.item()
     per = elapsed / steps
     ops = 2.0 * m * n * k
-    import statistics
-    med = statistics.median(s.elapsed_time(e) for s, e in ev) * 1e-3
+    med = clock.median_ms() * 1e-3
     return {"shape": [m, n, k], "n_gpus": world, "tops": ops / per / 1e12, "ms_per_step": per * 1e3,
             "median_step_ms_rank0": med * 1e3,
             "step": "int8_row_quant(X) + fused igemmlt+dequant on this rank's CB rows" +
@@ -505,14 +524,11 @@ def main():
 
     library = gemm_kernel_name(Mc, shard).startswith("hipBLASLt")
 
-    step_ev = []
+    clock = StepClock(args.steps)
 
     def step(record=False):
         # fused kernel: nested stats -> fp32 absmax once per step, shared by the chunks; library path:
         # gemm_4bit decodes them inside its dequantise launch
-        if record:
-            s0, e0 = _events()
-            s0.record()
         absmax = None if library else F._absmax_fp32(st)
         ev = []
 
@@ -530,8 +546,6 @@ def main():
             mm(X, Y)
         if record:
             kev.append(ev)
-            e0.record()
-            step_ev.append((s0, e0))
 
     # clock ramp: MI355X takes ~0.1-0.3 s of sustained MFMA load to reach its steady clock; run the
     # step untimed for --prewarm-ms before the W counted warmup steps (the timed region is unchanged)
@@ -549,8 +563,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
+    clock.mark()
+    for i in range(args.steps):
+        step(record=(i % STAGE_EVERY == 0))
+        clock.mark()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -573,8 +589,7 @@ def main():
     shard_flops = 2.0 * Mc * shard * K
     achieved = shard_flops / kern_s / 1e12
 
-    import statistics
-    median_step_ms = statistics.median(s.elapsed_time(e) for s, e in step_ev)
+    median_step_ms = clock.median_ms()
 
     extras = {}
     if not args.no_int8:     # every rank: it contains collectives when world > 1
