@@ -448,11 +448,12 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
                             "note": "median of 5; same inputs; outputs bit-identical (tests/test_cpu_path.py)"}}
 
 
-def gemm_kernel_name(m, n, k=K):
+def gemm_kernel_name(m, n, k=K, route=None):
     """Which kernel carries gemm_4bit's flops for m tokens x n features: from GEMM_4BIT_DEQUANT_MIN_ROWS
-    tokens the library GEMM after the dequantise kernel; below, gemm4bit.hip's 256x256 tile kernel when
-    the features are >= 256 and the grid (with split-K) has >= 128 workgroups, else the 128x128 one."""
-    if m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES:
+    tokens the library GEMM after the dequantise kernel (unless the measured route, `route`, is "fused");
+    below, gemm4bit.hip's 256x256 tile kernel when the features are >= 256 and the grid (with split-K) has
+    >= 128 workgroups, else the 128x128 one."""
+    if m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES and route != "fused":
         return "hipBLASLt bf16 GEMM (Cijk_*, via torch.matmul) after k_dequantize_4bit_stream<bf16,NF4>"
     ks = max(1, F.lib.cgemm_4bit_workspace_bytes(ct.c_int32(n), ct.c_int32(m), ct.c_int32(k)) // (4 * m * n))
     tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
@@ -556,6 +557,9 @@ def main():
         for c in range(chunks):
             F.gemm_4bit(X[c * Mc:(c + 1) * Mc], q, st, out=Y[c * Mc:(c + 1) * Mc], absmax=am)
         torch.cuda.synchronize()
+    # the route gemm_4bit measured for this shape on its first call (functional.GEMM_4BIT_ROUTE_TUNING)
+    kname = gemm_kernel_name(Mc, shard, route=F.gemm_4bit_measured_route(X[:Mc], st))
+    library = kname.startswith("hipBLASLt")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -614,7 +618,7 @@ def main():
         pmc = load_pmc_traffic()
         traffic = None
         pmc_extra = {}
-        if pmc and pmc.get("kernel") == gemm_kernel_name(Mc, shard) and pmc.get("shape") == [Mc, shard, K]:
+        if pmc and pmc.get("kernel") == kname and pmc.get("shape") == [Mc, shard, K]:
             traffic = pmc.get("hbm_bytes_per_launch")
             pmc_extra = {k: pmc[k] for k in ("mfma_busy_per_simd", "effective_clock_ghz") if k in pmc}
         line = {
@@ -640,7 +644,7 @@ def main():
                                        "output assembled)") if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                         "kernel": gemm_kernel_name(Mc, shard), "kernel_us": round(kern_s * 1e6, 2),
+                         "kernel": kname, "kernel_us": round(kern_s * 1e6, 2),
                          "flops_per_launch": shard_flops,
                          "dequantize_us": round(deq_s * 1e6, 2) if deq_s else None, **pmc_extra},
             "cpu_baseline": cpu,

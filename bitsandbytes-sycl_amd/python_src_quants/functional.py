@@ -735,8 +735,57 @@ GEMM_4BIT_WIDE_MAX_ROWS = 256
 # once and dotted with each row, whole K per workgroup, one launch, rows bit-identical to gemv_4bit on each row).
 GEMM_4BIT_GEMV_TOKENS = 4
 
+# Measured route for prefill shapes.  Where the static rule picks the dequantise + library pair (rows >=
+# GEMM_4BIT_DEQUANT_MIN_ROWS), the library's own solution choice can be far off for some shapes: torch's default
+# hipBLASLt heuristic runs 4096 x 11008 x 4096 (rows x out x in: the gate/up projection at 4096 tokens) at 0.87
+# PFLOP/s, where the fused kernel reaches 1.06 and the library itself 1.48 with a tuned solution
+# (profiles/lab/r02_lib_route.txt, r02_tunableop.txt).  So the first call of such a shape (per device, dtype and
+# statistics format) times both routes on its own operands (one warm call, best of two timed) and keeps the fused
+# kernel only when it wins by more than GEMM_4BIT_ROUTE_MARGIN; otherwise, and during HIP-graph capture, the
+# static rule stands.  The choice is cached for the process.  GEMM_4BIT_ROUTE_TUNING = False: static rule only.
+GEMM_4BIT_ROUTE_TUNING = True
+GEMM_4BIT_ROUTE_MARGIN = 0.05
+_ROUTES: dict = {}
+
 _DEQ_WS: dict = {}
 _DEQ_META: dict = {}
+
+
+def _route_key(A2: Tensor, state: QuantState, absmax: Optional[Tensor]):
+    return (A2.device.index, A2.shape[0], state.shape[0], state.shape[1], A2.dtype, state.quant_type, state.blocksize,
+            state.nested and absmax is None)
+
+
+def gemm_4bit_measured_route(A: Tensor, state: QuantState, absmax: Optional[Tensor] = None) -> Optional[str]:
+    """The measured route ("library" / "fused") cached for A's rows against this weight, or None when the shape
+    has not been measured (the static rule applies)."""
+    return _ROUTES.get(_route_key(A.reshape(-1, state.shape[1]), state, absmax))
+
+
+def _tuned_library_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor]) -> bool:
+    """True: keep the dequantise + library pair for this shape; False: the fused kernel measured faster."""
+    key = _route_key(A2, state, absmax)
+    route = _ROUTES.get(key)
+    if route is not None:
+        return route == "library"
+    if torch.cuda.is_current_stream_capturing():
+        return True
+    times = {}
+    for name in ("library", "fused"):
+        gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
+        best = None
+        for _ in range(2):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
+            e.record()
+            e.synchronize()
+            t = s.elapsed_time(e)
+            best = t if best is None else min(best, t)
+        times[name] = best
+    route = "fused" if times["fused"] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times["library"] else "library"
+    _ROUTES[key] = route
+    return route == "library"
 
 
 def _dequant_workspace(device, dtype, numel: int) -> Tensor:
@@ -784,7 +833,8 @@ def _gemm_4bit_tokens(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, ab
 
 
 def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = None,
-              absmax: Optional[Tensor] = None, events: Optional[list] = None, reuse_weight: bool = False) -> Tensor:
+              absmax: Optional[Tensor] = None, events: Optional[list] = None, reuse_weight: bool = False,
+              _route: Optional[str] = None) -> Tensor:
     """4-bit weight GEMM for any number of activation rows (the M>1 slot of cgemm_4bit_inference,
     ref:pythonInterface.cpp:377).  out[..., n] = A[..., :] @ W^T with W the dequantised [N, K] weight;
     replaces dequantize_4bit + F.linear (autograd/_functions.py:507).  Large problems (see
@@ -794,7 +844,8 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     that receives (name, start, end) torch.cuda.Event pairs around the launched stages.  reuse_weight:
     the caller runs several row chunks of one product against the same, unmodified weight (the chunked
     sharded forward); on the library path the workspace still holding this weight's dequantisation
-    from the previous call is used as is."""
+    from the previous call is used as is.  Prefill shapes on the library side of the static rule take the
+    measured route (GEMM_4BIT_ROUTE_TUNING); _route ("library" / "fused") forces one (internal)."""
     if not gemm_4bit_supported(A, state):
         raise ValueError("gemm_4bit: needs bf16/fp16 activations and in_features % 64 == 0")
     N, K = state.shape[0], state.shape[1]
@@ -807,6 +858,10 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
+    if _route is not None:
+        library = _route == "library"
+    elif library and rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and GEMM_4BIT_ROUTE_TUNING:
+        library = _tuned_library_route(A2, Bc, state, out.view(rows, N), absmax)
     if not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events):
         return out.view(*A.shape[:-1], N)
     if (absmax is None and not library and rows <= GEMM_4BIT_FEW_TOKENS and _nested_stats_in_kernel_ok(state)):

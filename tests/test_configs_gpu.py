@@ -93,3 +93,44 @@ def test_llama2_70b_shard(dev, name, n_out, k_in):
     _check_rows(Y, X, qs, part, n, k_in, sts.code, _sample_rows(M, dev, seed=n))
     # and the shard's packed bytes are the full weight's rows [rank*n, (rank+1)*n)
     assert torch.equal(qs.reshape(-1), q.reshape(-1)[rank * n * k_in // 2:(rank + 1) * n * k_in // 2])
+
+
+def test_measured_route_4096_tokens_gate_up(dev):
+    """The gate/up projection at 4096 tokens (11008 x 4096 weight), where torch's default hipBLASLt solution is
+    slow: the first call measures both routes (functional.GEMM_4BIT_ROUTE_TUNING) and caches one; both forced
+    routes and the routed call are within the oracle tolerance, the cache is stable, and a call under HIP-graph
+    capture neither measures nor fails."""
+    F = _F()
+    M, N, K = 4096, 11008, 4096
+    q, st = _quantized(N, K, dev, 77)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=torch.Generator(device=dev).manual_seed(7))
+    rows = _sample_rows(M, dev, n=128, seed=3)
+    am = F._absmax_fp32(st)
+    F._ROUTES.pop(F._route_key(X, st, None), None)
+    for route in ("library", "fused"):
+        Y = F.gemm_4bit(X, q, st, _route=route)
+        _check_rows(Y, X, q, am, N, K, st.code, rows)
+    Y = F.gemm_4bit(X, q, st)
+    first = F.gemm_4bit_measured_route(X, st)
+    assert first in ("library", "fused")
+    _check_rows(Y, X, q, am, N, K, st.code, rows)
+    F.gemm_4bit(X, q, st)
+    assert F.gemm_4bit_measured_route(X, st) == first
+    # capture: an unmeasured shape takes the static rule without timing anything
+    X2 = X[:3072].contiguous()
+    F._ROUTES.pop(F._route_key(X2, st, None), None)
+    out = torch.empty(3072, N, device=dev, dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        F.gemm_4bit(X2, q, st, out=out, _route="library")      # workspaces allocated outside the capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            F.gemm_4bit(X2, q, st, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    assert F.gemm_4bit_measured_route(X2, st) is None
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    _check_rows(out, X2, q, am, N, K, st.code, rows[rows < 3072])

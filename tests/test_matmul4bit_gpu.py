@@ -220,11 +220,13 @@ def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("qt", ["nf4", "fp4"])
-def test_gemm_4bit_library_path(dev, dtype, qt):
+def test_gemm_4bit_library_path(dev, dtype, qt, monkeypatch):
     """From GEMM_4BIT_DEQUANT_MIN_ROWS x GEMM_4BIT_DEQUANT_MIN_FEATURES gemm_4bit runs the reference's M > 1
     algorithm on the GPU: the HIP dequantise kernel into a workspace, then one library GEMM.  Bit-equal to
-    dequantize_4bit + torch.matmul, within the GEMM tolerance of the oracle, and close to the fused kernel."""
+    dequantize_4bit + torch.matmul, within the GEMM tolerance of the oracle, and close to the fused kernel.
+    (The static rule: the measured route is switched off here.)"""
     F = _F()
+    monkeypatch.setattr(F, "GEMM_4BIT_ROUTE_TUNING", False)
     M, N, K = 2048, 1024, 2048
     assert M >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and N >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES
     torch.manual_seed(17)
@@ -296,9 +298,10 @@ def test_gemm_4bit_asymmetric_identity(dev):
     assert torch.equal(Y, Wd.t().contiguous())
 
 
-def test_gemm_4bit_reuse_weight_chunks(dev):
+def test_gemm_4bit_reuse_weight_chunks(dev, monkeypatch):
     """Chunked forward on the library path: chunks after the first reuse the dequantised weight
     (reuse_weight); the result equals the unchunked call, and a different weight is never reused."""
+    monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
     F = _F()
     from python_src_quants.parallel import ColumnShardedLinear4bit
     M, N, K = 4096, 1024, 2048
@@ -316,9 +319,10 @@ def test_gemm_4bit_reuse_weight_chunks(dev):
     assert torch.equal(y2, torch.matmul(X[:2048], F.dequantize_4bit(q2, st2).t()))
 
 
-def test_gemm_4bit_library_path_two_streams(dev):
+def test_gemm_4bit_library_path_two_streams(dev, monkeypatch):
     """Two streams running the dequantise + library GEMM path concurrently on different weights each use
     their own weight workspace (keyed by stream): both results equal their single-stream values."""
+    monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
     F = _F()
     M, N, K = 2048, 2048, 1024
     torch.manual_seed(29)
@@ -437,6 +441,7 @@ def test_gemm_4bit_few_tokens_ragged_n(dev, nested, qt, bs, mnk):
 def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
     """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 forces the dequantise + library GEMM route for few tokens too (the few-token
     branch is not taken): the result equals dequantize_4bit + torch.matmul bit for bit."""
+    monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1)
     M, N, K = 8, 2048, 1024

@@ -39,11 +39,8 @@ def sweep():
         for M in (256, 512, 1024, 2048, 4096):
             X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
             Y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            F.GEMM_4BIT_DEQUANT_MIN_ROWS = 1 << 30
-            t_f = timeit(lambda: F.gemm_4bit(X, q, st, out=Y, absmax=am))
-            F.GEMM_4BIT_DEQUANT_MIN_ROWS = 1
-            F.GEMM_4BIT_DEQUANT_MIN_FEATURES = 1
-            t_l = timeit(lambda: F.gemm_4bit(X, q, st, out=Y, absmax=am))
+            t_f = timeit(lambda: F.gemm_4bit(X, q, st, out=Y, absmax=am, _route="fused"))
+            t_l = timeit(lambda: F.gemm_4bit(X, q, st, out=Y, absmax=am, _route="library"))
             t_d = timeit(lambda: F.dequantize_4bit(q, st, out=Wd))
             print(f"N={N:5d} M={M:5d}  fused {t_f:8.1f} us   dequant+matmul {t_l:8.1f} us   (dequant alone {t_d:6.1f})",
                   flush=True)

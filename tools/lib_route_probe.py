@@ -34,7 +34,6 @@ def t_us(fn, it=10):
 def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    base_rows = F.GEMM_4BIT_DEQUANT_MIN_ROWS
     for (m, n, k) in SHAPES:
         X = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
         W = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
@@ -43,20 +42,14 @@ def main():
         Y = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
 
         def fused():
-            F.GEMM_4BIT_DEQUANT_MIN_ROWS = 1 << 30
-            try:
-                F.gemm_4bit(X, q, st, out=Y)
-            finally:
-                F.GEMM_4BIT_DEQUANT_MIN_ROWS = base_rows
+            F.gemm_4bit(X, q, st, out=Y, _route="fused")
 
         def lib(name):
             def go():
                 torch.backends.cuda.preferred_blas_library(name)
-                F.GEMM_4BIT_DEQUANT_MIN_ROWS = 1
                 try:
-                    F.gemm_4bit(X, q, st, out=Y)
+                    F.gemm_4bit(X, q, st, out=Y, _route="library")
                 finally:
-                    F.GEMM_4BIT_DEQUANT_MIN_ROWS = base_rows
                     torch.backends.cuda.preferred_blas_library("cublaslt")
             return go
         arms = {"fused": fused, "lt": lib("cublaslt"), "rocblas": lib("cublas")}
