@@ -282,6 +282,7 @@ template <typename T>
 bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
                              int blocksize, int blocksize2, const float* code, T* out, int ldc, float* ws,
                              long long ws_bytes) {
+  if (launch_gemm_4bit_wk<T>(m, n, k, A, lda, B, ldb, st, blocksize, blocksize2, code, out, ldc)) return true;
   if (!skinny_applicable(m, n, k, lda, ldb, blocksize, A, B)) return false;
   const bool nested = st.q8 != nullptr;
   if (nested && (blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1)))) return false;

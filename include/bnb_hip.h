@@ -87,6 +87,11 @@ int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bnb_bf16* A, uns
                                            float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2);
 
+/* [additive, testing] few-token (1..32 activation rows) GEMM kernel choice: 0 = auto (the whole-K kernel,
+ * gemm4bit_wk.hip, no workspace, at <= 6 rows on weights of < 2 row tiles per CU; else the split-K kernel),
+ * 1 = the split-K kernel (gemm4bit_skinny.hip + its ordered reduce) only, 2 = the whole-K kernel wherever it fits */
+void cgemm_4bit_set_fewtoken_kernel(int which);
+
 /* [additive, testing] GEMV kernel choice: 0 = auto (the balanced-range kernel where the shape fits, else the
  * 4-waves-x-R-rows kernel), 1 = the 4-waves-x-R-rows kernel only; both give identical bits */
 void cgemv_4bit_set_kernel(int which);

@@ -577,3 +577,41 @@ def test_gemm_4bit_multirow_gemv_entry_declines(dev):
         F.GEMM_4BIT_GEMV_TOKENS = saved
     rms = Ys.float().pow(2).mean().sqrt().item()
     assert (Yg.float() - Ys.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Ys.float().abs().max().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("mnk", [(5, 1001, 2048), (8, 11008, 4096), (16, 4096, 11008), (24, 4099, 4096), (32, 1, 256),
+                                 (7, 300, 128), (17, 4096, 4096), (12, 28672 // 8, 8192)])
+def test_fewtoken_whole_k_and_split_k_kernels(dev, dtype, nested, mnk):
+    """The two few-token kernels, each forced (cgemm_4bit_set_fewtoken_kernel 2 / 1): the whole-K kernel (K split
+    over the workgroup's waves, summed in LDS in wave order, no workspace) and the split-K skinny kernel (+ ordered
+    reduce launch) -- each within the oracle tolerance, and the whole-K one deterministic across calls.  Covers one-block K
+    (fewer blocks than waves), ragged out_features, 1 and 2 token tiles, the 4- and 8-wave instances."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M * 31 + N)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64,
+                                    st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    saved = F.GEMM_4BIT_GEMV_TOKENS
+    F.GEMM_4BIT_GEMV_TOKENS = 1
+    outs = []
+    try:
+        for kern in (2, 1):
+            F.lib.cgemm_4bit_set_fewtoken_kernel(kern)
+            Y = F.gemm_4bit(X, q, st)
+            torch.cuda.synchronize()
+            assert F.lib.cget_last_error() == 0
+            frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
+            assert frac == 0.0, (kern, err)
+            outs.append(Y)
+        F.lib.cgemm_4bit_set_fewtoken_kernel(2)
+        assert torch.equal(outs[0], F.gemm_4bit(X, q, st))      # the whole-K kernel again: deterministic
+    finally:
+        F.lib.cgemm_4bit_set_fewtoken_kernel(0)
+        F.GEMM_4BIT_GEMV_TOKENS = saved
