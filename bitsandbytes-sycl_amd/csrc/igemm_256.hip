@@ -14,6 +14,8 @@
 #include "gemm_common.hpp"
 #include "int8_common.hpp"
 
+#include <algorithm>
+
 namespace bnb {
 
 typedef __attribute__((ext_vector_type(4))) int i32x4_t;
@@ -30,17 +32,27 @@ __device__ __forceinline__ const int8_t* chunk_ptr(const int8_t* P, long long ld
   return P + fmt_offset<F>(r, k, ld);    // 16 contiguous bytes for ROW / COL32 / AMPERE when k % 16 == 0
 }
 
-template <int AF, int BF, int EPI>
+// SPLIT (row-major A and B only): the grid is tiles x ksplit, workgroup `split` sums k-tiles [kb, kb + nk) of K / 128
+// and stores its int32 tile to ws[split][M][N]; k_igemm_splitk_reduce adds the splits (exact integer sums, so any
+// order gives the unsplit kernel's int32) and applies the epilogue.  For small tile grids: the column shards of the
+// multi-GPU step (N / 8 = 512 features: 16-32 tiles on 256 CUs).
+template <int AF, int BF, int EPI, bool SPLIT = false>
 __global__ void __launch_bounds__(J_THREADS, 1)
 k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restrict__ B, void* __restrict__ Cout,
             const float* __restrict__ row_scale, long long lda, long long ldb, long long ldc,
-            const float* __restrict__ rowStats, const float* __restrict__ colStats, const fp16_t* __restrict__ bias) {
+            const float* __restrict__ rowStats, const float* __restrict__ colStats, const fp16_t* __restrict__ bias,
+            int32_t* __restrict__ ws = nullptr, int ksplit_arg = 1) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[J_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   const int tilesN = (N + J_BN - 1) / J_BN, tilesM = (M + J_BM - 1) / J_BM;
-  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  const int ksplit = SPLIT ? ksplit_arg : 1;
+  const int ntiles = tilesN * tilesM;
+  // with split-K the split is the outer index, so an XCD's workgroups share one K range
+  const int wg_all = xcd_remap(blockIdx.x, ntiles * ksplit);
+  const int split = SPLIT ? wg_all / ntiles : 0;
+  const int wg = SPLIT ? wg_all - split * ntiles : wg_all;
   constexpr int GROUP = 4;
   const int group_span = GROUP * tilesN;
   const int first_m = (wg / group_span) * GROUP;
@@ -75,8 +87,10 @@ k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __r
     const unsigned off = min(t_lane + (unsigned)(((long long)kt * 4 + cb) * ldb) + 1024u * j, t_last);
     glds16(B + off, smem + 2 * J_TILE + buf * J_TILE + cb * 8192 + j * 1024);
   };
+  const int nk_all = K / J_BK;
+  const int kb = SPLIT ? (int)((long long)split * nk_all / ksplit) : 0;   // this split's first k-tile
   auto dma = [&](int kt, int buf) {
-    const long long k0 = (long long)kt * J_BK;
+    const long long k0 = (long long)(kb + kt) * J_BK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       glds16(chunk_ptr<AF>(A, lda, arow[i], k0 + kslot[i]), smem + buf * J_TILE + (4 * wave + i) * 1024);
@@ -136,7 +150,7 @@ k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __r
         acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4_t, a[i]), __builtin_bit_cast(i32x4_t, b[j]),
                                                           acc[i][j], 0, 0, 0);
   };
-  const int nk = K / J_BK;
+  const int nk = SPLIT ? (int)((long long)(split + 1) * nk_all / ksplit) - kb : nk_all;
   dma(0, 0);
   if (nk > 1) {
     dma(1, 1);
@@ -161,6 +175,22 @@ k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __r
 
   // ---- epilogues (C/D: col = lane&15, row = 4*(lane>>4) + r)
   const int grow0 = m0 + 128 * wm, gcol0 = n0 + 64 * wn;
+  if constexpr (SPLIT) {
+    int32_t* wsp = ws + (long long)split * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = grow0 + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = gcol0 + 16 * j + (lane & 15);
+          if (col < N) wsp[(long long)row * N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
   if constexpr (EPI == EPI_F16_ROW_DEQUANT) {
     uint8_t* ep = smem + wave * (128 * J_EPI_STRIDE);
     float cs[4], bv[4];
@@ -223,10 +253,65 @@ k_igemm_256(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __r
   }
 }
 
+// out[r, c] = EPI(sum_s ws[s][r][c]): int32 sums (exact), then the fused mm_dequant to fp16 or the int32 store.
+// 4 columns per thread (N % 4 == 0: 16-B loads), else one.
+template <int EPI>
+__global__ void __launch_bounds__(256)
+k_igemm_splitk_reduce(const int32_t* __restrict__ ws, int ksplit, int M, int N, void* __restrict__ Cout, long long ldc,
+                      const float* __restrict__ rowStats, const float* __restrict__ colStats,
+                      const fp16_t* __restrict__ bias) {
+  const long long mn = (long long)M * N;
+  const int V = (N & 3) == 0 ? 4 : 1;
+  const long long i0 = (long long)V * ((long long)blockIdx.x * 256 + threadIdx.x);
+  if (i0 >= mn) return;
+  int32_t v[4] = {0, 0, 0, 0};
+  if (V == 4) {
+    for (int s = 0; s < ksplit; ++s) {
+      const int4 p = *reinterpret_cast<const int4*>(ws + s * mn + i0);
+      v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+    }
+  } else {
+    for (int s = 0; s < ksplit; ++s) v[0] += ws[s * mn + i0];
+  }
+  const long long r = i0 / N, c0 = i0 - r * N;
+  for (int e = 0; e < V; ++e) {
+    const long long c = c0 + e;
+    if constexpr (EPI == EPI_F16_ROW_DEQUANT) {
+      reinterpret_cast<fp16_t*>(Cout)[r * ldc + c] =
+          mm_dequant_value(v[e], rowStats[r], colStats[c], bias ? (float)bias[c] : 0.0f);
+    } else {
+      reinterpret_cast<int32_t*>(Cout)[r * ldc + c] = v[e];
+    }
+  }
+}
+
+static int g_igemm_splitk = -1;   // < 0: auto; 1 = never split; >= 2: force that factor where it applies (tests)
+
+// Split-K factor for a row-major 256-tile problem: enough workgroups for the 256 CUs when the output has fewer
+// than ~200 tiles, with at least 8 k-tiles (1024 k) per split, at most 16 splits.
+int igemm_splitk_factor(int m, int n, int k) {
+  if (k % J_BK != 0 || m < 256 || n < 256) return 1;
+  const long long tiles = (long long)((m + J_BM - 1) / J_BM) * ((n + J_BN - 1) / J_BN);
+  int ks;
+  if (g_igemm_splitk >= 1) {
+    ks = g_igemm_splitk;
+  } else {
+    if (tiles >= 200) return 1;
+    ks = (int)((256 + tiles / 2) / tiles);
+  }
+  ks = std::min(ks, std::max(1, (k / J_BK) / 8));
+  return std::max(1, std::min(ks, 16));
+}
+
+long long igemm_workspace_bytes(int m, int n, int k) {
+  const int ks = igemm_splitk_factor(m, n, k);
+  return ks > 1 ? (long long)ks * m * n * (long long)sizeof(int32_t) : 0;
+}
+
 template <int AF, int BF, int EPI>
 bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale,
                       long long lda, long long ldb, long long ldc, const float* rowStats, const float* colStats,
-                      const fp16_t* bias) {
+                      const fp16_t* bias, int32_t* ws, long long ws_bytes) {
   if constexpr (AF == TURING) {
     return false;                                                  // A in 4-byte runs: register-staged kernel
   } else {
@@ -234,8 +319,22 @@ bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, voi
     if ((AF == ROW && lda % 16) || (BF == ROW && ldb % 16) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return false;
     if (BF == TURING && (ldb % 256 || ldb < 32LL * n || (long long)(k / 32) * ldb >= (1LL << 32))) return false;
     const long long tiles = (long long)((m + J_BM - 1) / J_BM) * ((n + J_BN - 1) / J_BN);
+    if constexpr (AF == ROW && BF == ROW && (EPI == EPI_F16_ROW_DEQUANT || EPI == EPI_I32_ROW)) {
+      const int ks = igemm_splitk_factor(m, n, k);
+      if (ks > 1 && ws != nullptr && ((uintptr_t)ws & 15) == 0 &&
+          (long long)ks * m * n * (long long)sizeof(int32_t) <= ws_bytes) {
+        hipLaunchKernelGGL((k_igemm_256<AF, BF, EPI, true>), dim3((unsigned)(tiles * ks)), dim3(J_THREADS), 0,
+                           current_stream(), m, n, k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias, ws,
+                           ks);
+        const long long mn = (long long)m * n;
+        const long long threads = (n % 4 == 0) ? mn / 4 : mn;
+        hipLaunchKernelGGL((k_igemm_splitk_reduce<EPI>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                           current_stream(), ws, ks, m, n, C, ldc, rowStats, colStats, bias);
+        return true;
+      }
+    }
     hipLaunchKernelGGL((k_igemm_256<AF, BF, EPI>), dim3((unsigned)tiles), dim3(J_THREADS), 0, current_stream(), m, n,
-                       k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias);
+                       k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias, nullptr, 1);
     return true;
   }
 }
@@ -243,7 +342,7 @@ bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, voi
 #define BNB_INST(AF, BF, EPI)                                                                                      \
   template bool launch_igemm_256<AF, BF, EPI>(int, int, int, const int8_t*, const int8_t*, void*, const float*,    \
                                               long long, long long, long long, const float*, const float*,         \
-                                              const fp16_t*);
+                                              const fp16_t*, int32_t*, long long);
 BNB_INST(ROW, ROW, EPI_F16_ROW_DEQUANT)
 BNB_INST(ROW, ROW, EPI_I32_ROW)
 BNB_INST(COL32, AMPERE, EPI_I32_COL32)
@@ -255,3 +354,8 @@ BNB_INST(COL32, TURING, EPI_I8_COL32_ROWSCALE)
 #undef BNB_INST
 
 }  // namespace bnb
+
+extern "C" {
+// [additive, testing] int8 split-K factor: -1 = auto, 1 = never split, >= 2 = force where it applies
+void cigemm_set_splitk(int ks) { bnb::g_igemm_splitk = ks; }
+}

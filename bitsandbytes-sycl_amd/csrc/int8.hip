@@ -615,11 +615,13 @@ static int g_igemm_tile = 0;   // 0 = auto, 128 = force the 128x128 register-sta
 template <int AF, int BF, int EPI>
 static int launch_igemm(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale, long long lda,
                         long long ldb, long long ldc, const float* rowStats = nullptr, const float* colStats = nullptr,
-                        const fp16_t* bias = nullptr) {
+                        const fp16_t* bias = nullptr, int32_t* ws = nullptr, long long ws_bytes = 0) {
   if (m <= 0 || n <= 0 || k <= 0) return 0;
-  // large problems: 256x256 LDS-DMA kernel (igemm_256.hip); small / col_turing / ragged-k: 128x128 here
+  // large problems: 256x256 LDS-DMA kernel (igemm_256.hip; split-K over ws for small tile grids); small /
+  // col_turing / ragged-k: 128x128 here
   if (g_igemm_tile != 128 &&
-      launch_igemm_256<AF, BF, EPI>(m, n, k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias)) {
+      launch_igemm_256<AF, BF, EPI>(m, n, k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias, ws,
+                                    ws_bytes)) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_error((int)e, "igemmlt launch"); return 1; }
     return 0;
@@ -750,6 +752,20 @@ int cigemmlt_row_dequant_fp16(int m, int n, int k, const int8_t* A, const int8_t
 int cigemm_row_i32(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc) {
   return launch_igemm<ROW, ROW, EPI_I32_ROW>(m, n, k, A, B, out, nullptr, lda, ldb, ldc);
 }
+// Additive: the two row-major entry points with a caller workspace (size: cigemmlt_workspace_bytes) that lets
+// small tile grids -- the column shards of the multi-GPU step -- run split-K; the result is the same bits.
+int cigemmlt_row_dequant_ws_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, fp16_t* out,
+                                 const float* rowStats, const float* colStats, const fp16_t* bias, int lda, int ldb,
+                                 int ldc, int32_t* workspace, long long workspace_bytes) {
+  return launch_igemm<ROW, ROW, EPI_F16_ROW_DEQUANT>(m, n, k, A, B, out, nullptr, lda, ldb, ldc, rowStats, colStats,
+                                                     bias, workspace, workspace_bytes);
+}
+int cigemm_row_i32_ws(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc,
+                      int32_t* workspace, long long workspace_bytes) {
+  return launch_igemm<ROW, ROW, EPI_I32_ROW>(m, n, k, A, B, out, nullptr, lda, ldb, ldc, nullptr, nullptr, nullptr,
+                                             workspace, workspace_bytes);
+}
+long long cigemmlt_workspace_bytes(int m, int n, int k) { return igemm_workspace_bytes(m, n, k); }
 
 void cdequant_mm_int32_fp16(int* A, float* rowStats, float* colStats, fp16_t* out, float* newRowStats,
                             float* newcolStats, fp16_t* bias, int numRows, int numCols) {

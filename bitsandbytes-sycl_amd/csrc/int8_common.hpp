@@ -44,9 +44,13 @@ __device__ __forceinline__ fp16_t mm_dequant_value(int32_t acc, float rs, float 
 enum Epi { EPI_I32_COL32 = 0, EPI_I8_COL32 = 1, EPI_I8_COL32_ROWSCALE = 2, EPI_F16_ROW_DEQUANT = 3, EPI_I32_ROW = 4 };
 
 // 256x256-tile int8 GEMM (igemm_256.hip); returns false when the shape/layout is not covered
+// ws / ws_bytes: a caller workspace that lets small tile grids of row-major operands run split-K (int32 partials,
+// summed exactly by a reduce launch that also applies the epilogue); NULL or too small: no split
 template <int AF, int BF, int EPI>
 bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale,
                       long long lda, long long ldb, long long ldc, const float* rowStats, const float* colStats,
-                      const fp16_t* bias);
+                      const fp16_t* bias, int32_t* ws = nullptr, long long ws_bytes = 0);
+int igemm_splitk_factor(int m, int n, int k);
+long long igemm_workspace_bytes(int m, int n, int k);
 
 }  // namespace bnb

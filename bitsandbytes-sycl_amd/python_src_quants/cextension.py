@@ -36,9 +36,11 @@ class BNBNativeLibrary:
         lib.cget_stream.restype = ct.c_void_p
         lib.cget_last_error_message.restype = ct.c_char_p
         lib.cgemm_4bit_workspace_bytes.restype = ct.c_longlong
+        lib.cigemmlt_workspace_bytes.restype = ct.c_longlong
         for name in ("cigemmlt_turing_32", "cigemmlt_turing_8", "cigemmlt_turing_8_rowscale",
                      "cigemmlt_ampere_32", "cigemmlt_ampere_8", "cigemmlt_ampere_8_rowscale",
-                     "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cget_last_error", "cget_abi_version",
+                     "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cigemmlt_row_dequant_ws_fp16",
+                     "cigemm_row_i32_ws", "cget_last_error", "cget_abi_version",
                      "cgemm_4bit_inference_naive_nested_fp16", "cgemm_4bit_inference_naive_nested_bf16",
                      "cdequantize_blockwise_nested_fp16_fp4", "cdequantize_blockwise_nested_fp16_nf4",
                      "cdequantize_blockwise_nested_bf16_fp4", "cdequantize_blockwise_nested_bf16_nf4",

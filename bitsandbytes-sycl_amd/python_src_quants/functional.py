@@ -1097,11 +1097,15 @@ def igemmlt_dequant(CA: Tensor, CB: Tensor, row_stats: Tensor, col_stats: Tensor
     CBc = CB.contiguous()
     if out is None:
         out = torch.empty((m, n), dtype=torch.float16, device=CA.device)
+    # small tile grids (the column shards of the multi-GPU step) run split-K through the grow-only workspace
+    ws_bytes = int(lib.cigemmlt_workspace_bytes(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k)))
+    ws = _gemm_workspace(CA.device, ws_bytes)
     prev_device = pre_call(CA.device)
     is_on_gpu([CA2, CBc, row_stats, col_stats, out, bias])
-    err = lib.cigemmlt_row_dequant_fp16(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(CA2), get_ptr(CBc),
-                                        get_ptr(out), get_ptr(row_stats), get_ptr(col_stats), get_ptr(bias),
-                                        ct.c_int32(k), ct.c_int32(k), ct.c_int32(n))
+    err = lib.cigemmlt_row_dequant_ws_fp16(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(CA2), get_ptr(CBc),
+                                           get_ptr(out), get_ptr(row_stats), get_ptr(col_stats), get_ptr(bias),
+                                           ct.c_int32(k), ct.c_int32(k), ct.c_int32(n), get_ptr(ws),
+                                           ct.c_longlong(ws_bytes))
     if err:
         raise Exception("igemmlt ran into an error!")
     post_call(prev_device)
@@ -1114,10 +1118,13 @@ def igemm_rowmajor(A: Tensor, B: Tensor, out: Optional[Tensor] = None) -> Tensor
     n = B.shape[0]
     if out is None:
         out = torch.empty((m, n), dtype=torch.int32, device=A.device)
+    ws_bytes = int(lib.cigemmlt_workspace_bytes(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k)))
+    ws = _gemm_workspace(A.device, ws_bytes)
+    Ac, Bc = A.contiguous(), B.contiguous()
     prev_device = pre_call(A.device)
     is_on_gpu([A, B, out])
-    err = lib.cigemm_row_i32(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(A.contiguous()),
-                             get_ptr(B.contiguous()), get_ptr(out), ct.c_int32(k), ct.c_int32(k), ct.c_int32(n))
+    err = lib.cigemm_row_i32_ws(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), get_ptr(Ac), get_ptr(Bc), get_ptr(out),
+                                ct.c_int32(k), ct.c_int32(k), ct.c_int32(n), get_ptr(ws), ct.c_longlong(ws_bytes))
     if err:
         raise Exception("igemm ran into an error!")
     post_call(prev_device)

@@ -184,6 +184,18 @@ int cigemmlt_ampere_8(int m, int n, int k, const int8_t* A, const int8_t* B, voi
 int cigemmlt_row_dequant_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, bnb_fp16* out, const float* rowStats,
                               const float* colStats, const bnb_fp16* bias, int lda, int ldb, int ldc);
 int cigemm_row_i32(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc);
+/* [additive] the two row-major int8 entry points with a caller-owned workspace (bytes: cigemmlt_workspace_bytes;
+ * 0 = no split for this shape) that lets small tile grids (the column shards of the multi-GPU step) run split-K:
+ * int32 partials summed exactly by a second launch that applies the epilogue -- the same bits as without it.  A NULL
+ * or smaller workspace runs unsplit. */
+int cigemmlt_row_dequant_ws_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, bnb_fp16* out,
+                                 const float* rowStats, const float* colStats, const bnb_fp16* bias, int lda, int ldb,
+                                 int ldc, int32_t* workspace, long long workspace_bytes);
+int cigemm_row_i32_ws(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb,
+                      int ldc, int32_t* workspace, long long workspace_bytes);
+long long cigemmlt_workspace_bytes(int m, int n, int k);
+/* [additive, testing] int8 split-K factor: -1 = auto, 1 = never, >= 2 = force where it applies */
+void cigemm_set_splitk(int ks);
 /* [additive, testing] force the int8 GEMM tile kernel: 0 = auto (256x256 when it applies), 128 = 128x128 */
 void cigemm_set_tile(int tile);
 

@@ -243,3 +243,37 @@ def test_igemmlt_turing_abi_all_epilogues(dev, mnk):
     assert rc == 0
     got = ref.untransform(out.cpu().numpy(), m, n, "col32")
     assert np.array_equal(got, ref.igemmlt_int8_out(A, B, scale.cpu().numpy()))
+
+
+@pytest.mark.parametrize("mnk", [(4096, 512, 11008), (2048, 512, 11008), (2048, 1024, 4096), (4096, 2048, 11008),
+                                 (300, 258, 2048), (513, 777, 3072)])
+def test_igemm_split_k_exact(dev, mnk):
+    """Split-K over a workspace for small 256-tile grids (the column shards of the multi-GPU step): the int32
+    partials are summed exactly, so the int32 result equals the exact product (fp64 GPU matmul) and the fused
+    dequant equals the unsplit kernel's bits; auto factor, forced factors and the unsplit kernel compared."""
+    F = _F()
+    m, n, k = mnk
+    g = torch.Generator(device=dev).manual_seed(m + n)
+    A = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8, generator=g)
+    B = torch.randint(-127, 128, (n, k), device=dev, dtype=torch.int8, generator=g)
+    exp = (A.double() @ B.double().T).round().to(torch.int64).to(torch.int32)
+    rs = torch.rand(m, device=dev, generator=g) * 2 + 0.5
+    cs = torch.rand(n, device=dev, generator=g) * 2 + 0.5
+    bias = torch.randn(n, device=dev, generator=g).half()
+    outs32, outs16 = [], []
+    try:
+        for ks in (1, -1, 3, 16):
+            F.lib.cigemm_set_splitk(ks)
+            outs32.append(F.igemm_rowmajor(A, B))
+            outs16.append(F.igemmlt_dequant(A, B, rs, cs, bias=bias))
+            torch.cuda.synchronize()
+            assert F.lib.cget_last_error() == 0
+    finally:
+        F.lib.cigemm_set_splitk(-1)
+    for o in outs32:
+        assert torch.equal(o, exp)
+    for o in outs16[1:]:
+        assert torch.equal(o.view(torch.int16), outs16[0].view(torch.int16))
+    if m >= 256 and n >= 256 and k % 128 == 0:
+        tiles = ((m + 255) // 256) * ((n + 255) // 256)
+        assert (F.lib.cigemmlt_workspace_bytes(m, n, k) > 0) == (tiles < 200)
