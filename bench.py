@@ -216,10 +216,10 @@ def bench_decode_gemv(dev, iters=30):
     return res
 
 
-def bench_few_token_gemm(dev, iters=30, tokens=(2, 4, 8, 16, 32)):
+def bench_few_token_gemm(dev, iters=30, tokens=(2, 4, 8, 16, 32, 64)):
     """Batched decode / short prefill on the config-2 weight (11008 x 4096 NF4, nested statistics, the
     Linear4bit default): gemm_4bit with 2..4 activation rows runs the multi-row GEMV (gemv4bit_tok.hip, one
-    launch), 5..32 the weight-streaming MFMA kernel (gemm4bit_skinny.hip, + its ordered split-K reduce).  14 rotating weight copies, HIP-graph replay;
+    launch), 5..64 the weight-streaming MFMA kernel (gemm4bit_skinny.hip, + its ordered split-K reduce).  14 rotating weight copies, HIP-graph replay;
     GB/s over the algorithmic bytes (packed weights + nested stats + activations + output)."""
     n_out, k_in, copies = 11008, 4096, 14
     g = torch.Generator(device=dev).manual_seed(3)
@@ -229,7 +229,7 @@ def bench_few_token_gemm(dev, iters=30, tokens=(2, 4, 8, 16, 32)):
         ws.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True))
         del W
     res = {"shape": [None, n_out, k_in],
-           "path": "2..4 rows: k_gemv_4bit_tok; 5..32 rows: k_gemm_4bit_skinny (+ k_skinny_reduce)"}
+           "path": "2..4 rows: k_gemv_4bit_tok; 5..64 rows: k_gemm_4bit_skinny (+ k_skinny_reduce)"}
     for m in tokens:
         x = torch.randn(m, k_in, device=dev, dtype=torch.bfloat16, generator=g)
         out = torch.empty(m, n_out, device=dev, dtype=torch.bfloat16)

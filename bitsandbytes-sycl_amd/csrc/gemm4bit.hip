@@ -186,7 +186,7 @@ void gemm_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* a
     set_error(1, "gemm_4bit: requires k % 64 == 0, lda % 8 == 0, ldb % 16 == 0, 16-B aligned A/B, blocksize >= 64");
     return;
   }
-  // few tokens (<= 32, SK_MAX_TOKENS): the weight-streaming kernel (gemm4bit_skinny.hip)
+  // few tokens (<= 64, SK_MAX_TOKENS): the weight-streaming kernels (gemm4bit_skinny.hip, gemm4bit_wk.hip)
   if (g_tile_override == 0) {
     const SkStats st{absmax, nullptr, nullptr, nullptr, nullptr, 0, 0};
     if (launch_gemm_4bit_skinny<T>(m, n, k, A, lda, B, ldb, st, blocksize, 0, datatype, out, ldc, ws, ws_bytes)) {

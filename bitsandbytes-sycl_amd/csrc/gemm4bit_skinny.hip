@@ -1,4 +1,4 @@
-// Few-token 4-bit weight GEMM (batched decode / short prefill, 2..32 activation rows) for gfx950.
+// Few-token 4-bit weight GEMM (batched decode / short prefill, 2..64 activation rows) for gfx950.
 //
 // Same slot and semantics as gemm4bit.hip (cgemm_4bit_inference*, ref:sycl/pythonInterface.cpp:377-378;
 // the M > 1 path it replaces is dequantize_4bit + F.linear, ref:autograd/_functions.py:491-507): every
@@ -36,7 +36,7 @@ namespace bnb {
 #define SK_STAMP(i)
 #endif
 
-constexpr int SK_THREADS = 256, SK_ROWS = 64, SK_LUTC = LUTC_DEF, SK_MAX_TOKENS = 32;
+constexpr int SK_THREADS = 256, SK_ROWS = 64, SK_LUTC = LUTC_DEF, SK_MAX_TOKENS = 64;
 
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -254,10 +254,12 @@ k_skinny_reduce(const float* __restrict__ ws, int nsplit, int M, int N, T* __res
 }
 
 // Blocks of 128 k per workgroup: the activation slice ((NB + 1) x 16 MT rows x 256 B = 44 / 48 KiB at MT 1 / 2,
-// plus the pair table and code2: 47 / 51 KiB in all) lets three workgroups fit a CU; all of a workgroup's weights are in flight at once (NB x 16 B per lane).
-template <int MT> constexpr int skinny_nb() { return MT == 1 ? 10 : 5; }
+// plus the pair table and code2: 47 / 51 KiB in all) lets three workgroups fit a CU; at MT 4 (33..64 rows) three
+// blocks, 64 KiB + 3 KiB, two per CU.  All of a workgroup's weights are in flight at once (NB x 16 B per lane).
+template <int MT> constexpr int skinny_nb() { return MT == 1 ? 10 : (MT == 2 ? 5 : 3); }
 
-static int skinny_tiles(int n) { return (n + 15) / 16; }
+// 16-token MFMA tiles held: 1, 2, or 4 (33..64 rows)
+static int skinny_tiles(int n) { return n <= 16 ? 1 : (n <= 32 ? 2 : 4); }
 
 bool skinny_applicable(int m, int n, int k, int lda, int ldb, int blocksize, const void* A, const void* B) {
   return n >= 1 && n <= SK_MAX_TOKENS && m >= 1 && k >= 128 && k % 128 == 0 && blocksize >= 64 &&
@@ -266,7 +268,8 @@ bool skinny_applicable(int m, int n, int k, int lda, int ldb, int blocksize, con
 }
 
 int skinny_splits(int n, int k) {
-  const int nbw = skinny_tiles(n) == 1 ? skinny_nb<1>() : skinny_nb<2>();
+  const int mt = skinny_tiles(n);
+  const int nbw = mt == 1 ? skinny_nb<1>() : (mt == 2 ? skinny_nb<2>() : skinny_nb<4>());
   return (k / 128 + nbw - 1) / nbw;
 }
 
@@ -299,10 +302,12 @@ bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uin
   const int mt = skinny_tiles(n);
   if (nested) {
     if (mt == 1) go(k_gemm_4bit_skinny<T, 1, skinny_nb<1>(), true>);
-    else go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), true>);
+    else if (mt == 2) go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), true>);
+    else go(k_gemm_4bit_skinny<T, 4, skinny_nb<4>(), true>);
   } else {
     if (mt == 1) go(k_gemm_4bit_skinny<T, 1, skinny_nb<1>(), false>);
-    else go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), false>);
+    else if (mt == 2) go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), false>);
+    else go(k_gemm_4bit_skinny<T, 4, skinny_nb<4>(), false>);
   }
   if (s > 1) {
     const long long mn = (long long)m * n;

@@ -82,7 +82,7 @@ template <typename T>
 void launch_gemm_4bit_256(int m, int n, int k, const T* A, const uint8_t* B, const float* absmax, const float* datatype,
                           T* out, int lda, int ldb, int ldc, int blocksize, float* ws, int ksplit);
 
-// Few-token kernel (gemm4bit_skinny.hip): 1..32 activation rows (SK_MAX_TOKENS), K % 128 == 0.  Statistics either plain
+// Few-token kernel (gemm4bit_skinny.hip): 1..64 activation rows (SK_MAX_TOKENS), K % 128 == 0.  Statistics either plain
 // fp32 absmax or nested (q8 + code2 + absmax2 + offset, decoded in-kernel).
 struct SkStats {
   const float* absmax;

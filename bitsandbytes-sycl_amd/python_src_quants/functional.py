@@ -722,9 +722,11 @@ def _gemm_workspace(device, nbytes: int) -> Optional[Tensor]:
 # 4096 x 1024 108.7 vs 95.0; 1024 x 4096 108.2 vs 106.2; 512 x 4096 67.6 vs 80.4; 4096 x 512 69.6 vs 70.8.
 GEMM_4BIT_DEQUANT_MIN_ROWS = 2048
 GEMM_4BIT_DEQUANT_MIN_FEATURES = 1024
-# Up to this many activation rows the C side runs the weight-streaming kernel (gemm4bit_skinny.hip);
-# with nested statistics the Python side calls its one-launch entry point directly.
-GEMM_4BIT_FEW_TOKENS = 32
+# Up to this many activation rows the C side runs the weight-streaming kernel (gemm4bit_skinny.hip; 33..64 rows on
+# its 4-tile instance, round 2: 11008 x 4096 at 33..64 rows 43.7 -> 27.3..31.2 us against the library pair,
+# 4096 x 4096 18.4..21.0 -> 15.2..18.1 us against the tile kernels, profiles/lab/r02_fewtoken_64rows.txt); with
+# nested statistics the Python side calls its one-launch entry point directly.
+GEMM_4BIT_FEW_TOKENS = 64
 # Between GEMM_4BIT_FEW_TOKENS and this many rows, weights at least twice as wide (out features) as deep (in
 # features) also take the library pair: its 64-row tiles cover the wide output where the fused kernel's 256-wide
 # tile grid needs split-K (tools/smallm_sweep.py, profiles/lab/r02_routing.txt, graph replay, us fused vs library:

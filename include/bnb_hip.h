@@ -87,7 +87,7 @@ int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bnb_bf16* A, uns
                                            float* code2, float* absmax2, float* offset, float* datatype, bnb_bf16* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2);
 
-/* [additive, testing] few-token (1..32 activation rows) GEMM kernel choice: 0 = auto (the whole-K kernel,
+/* [additive, testing] few-token (1..64 activation rows; the whole-K kernel 1..32) GEMM kernel choice: 0 = auto (the whole-K kernel,
  * gemm4bit_wk.hip, no workspace, at <= 6 rows on weights of < 2 row tiles per CU; else the split-K kernel),
  * 1 = the split-K kernel (gemm4bit_skinny.hip + its ordered reduce) only, 2 = the whole-K kernel wherever it fits */
 void cgemm_4bit_set_fewtoken_kernel(int which);
@@ -119,11 +119,11 @@ void cgemm_4bit_inference_code_ws_bf16(int m, int n, int k, bnb_bf16* A, unsigne
                                        float* datatype, bnb_bf16* out, int lda, int ldb, int ldc, int blocksize,
                                        float* workspace, long long workspace_bytes);
 long long cgemm_4bit_workspace_bytes(int m, int n, int k);
-/* [additive] few tokens (n <= 32, k % 128 == 0): the weight-streaming kernel with compressed statistics
+/* [additive] few tokens (n <= 64, k % 128 == 0): the weight-streaming kernel with compressed statistics
  * (absmax_q uint8 codes, code2 256-entry map, absmax2 per blocksize2 codes, offset: one fp32 on the
  * device) decoded in-kernel -- replaces the absmax decode launch + GEMM of the M > 1 path
  * (ref:functional.py:1346-1350 + autograd/_functions.py:507).  The plain-absmax calls above use the
- * same kernel for n <= 32 when the workspace fits.  Returns 0 when launched, 1 when the shape,
+ * same kernel for n <= 64 when the workspace fits.  Returns 0 when launched, 1 when the shape,
  * alignment or workspace does not fit (the caller then decodes absmax and uses the _ws entry points). */
 int cgemm_4bit_inference_nested_ws_fp16(int m, int n, int k, bnb_fp16* A, unsigned char* B, unsigned char* absmax_q,
                                         float* code2, float* absmax2, float* offset, float* datatype, bnb_fp16* out,

@@ -348,8 +348,8 @@ def test_gemm_4bit_library_path_two_streams(dev, monkeypatch):
 @pytest.mark.parametrize("mnk", [(2, 11008, 4096), (3, 300, 1152), (16, 4096, 11008), (17, 1000, 2048),
                                  (33, 64, 128), (48, 520, 640), (64, 4096, 4096), (64, 11008, 4096)])
 def test_gemm_4bit_few_tokens_vs_oracle(dev, dtype, nested, mnk):
-    """1..32 activation rows (batched decode, short prefill) run the weight-streaming kernel; 33..64 the tile kernels
-    (gemm4bit_skinny.hip): same dequantised weights, fp32 sums split over K in split order.  Nested
+    """1..64 activation rows (batched decode, short prefill) run the weight-streaming kernel (gemm4bit_skinny.hip;
+    33..64 rows on its 4-tile instance): same dequantised weights, fp32 sums split over K in split order.  Nested
     statistics are decoded in the kernel.  Same tolerance as the tile kernels; ragged rows, one-block K,
     a tail chunk (K = 11008 = 86 blocks) and single-split shapes."""
     F = _F()
@@ -397,7 +397,7 @@ def test_gemm_4bit_few_tokens_nested_matches_plain(dev):
 def test_gemm_4bit_few_tokens_entry_point_declines(dev):
     """The one-launch entry point returns 1 (nothing launched) when the shape does not fit it."""
     F = _F()
-    M, N, K = 33, 256, 1024                     # > 32 tokens (SK_MAX_TOKENS)
+    M, N, K = 65, 256, 1024                     # > 64 tokens (SK_MAX_TOKENS)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     q, st = F.quantize_4bit((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16), blocksize=64,
                             quant_type="nf4", compress_statistics=True)

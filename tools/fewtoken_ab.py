@@ -2,7 +2,9 @@
 (gemm4bit_wk.hip, forced: cgemm_4bit_set_fewtoken_kernel(2)) and the split-K skinny kernel + its reduce launch
 (1) -- on the Llama-2-7B weights (nested NF4 bs 64), 14 rotating weight copies per shape (> the 256 MB
 MALL for the big ones), HIP-graph replay, interleaved rounds; medians.
-Usage: python tools/fewtoken_ab.py [tokens ...]"""
+Usage: python tools/fewtoken_ab.py [tokens ...]
+       FEWTOKEN_ROUTE=1 python tools/fewtoken_ab.py 33 48 64   (instead: the split-K kernel's 33..64-row instance
+       against the route gemm_4bit took there before it, GEMM_4BIT_FEW_TOKENS = 32)"""
 import os
 import sys
 
@@ -49,15 +51,20 @@ def main():
             x = torch.randn(m, k_in, device=dev, dtype=torch.bfloat16, generator=gen)
             out = torch.empty(m, n_out, device=dev, dtype=torch.bfloat16)
             calls = [(lambda q=q, st=st: F.gemm_4bit(x, q, st, out=out)) for q, st in ws]
-            res = {2: [], 1: []}
+            route = os.environ.get("FEWTOKEN_ROUTE") == "1"
+            arms = ((1, "split-K 64-row"), (0, "previous route")) if route else ((2, "whole-K"), (1, "split-K"))
+            res = {a: [] for a, _ in arms}
             for _ in range(5):
-                for kern in (2, 1):
-                    F.lib.cgemm_4bit_set_fewtoken_kernel(kern)
+                for kern, _ in arms:
+                    if route:
+                        F.GEMM_4BIT_FEW_TOKENS = 64 if kern == 1 else 32
+                    else:
+                        F.lib.cgemm_4bit_set_fewtoken_kernel(kern)
                     res[kern].append(graph_time(calls))
             F.lib.cgemm_4bit_set_fewtoken_kernel(0)
             nbytes = nbytes_w + m * k_in * 2 + m * n_out * 2
             line = f"{n_out}x{k_in} tokens {m:3d}:"
-            for kern, name in ((2, "whole-K"), (1, "split-K")):
+            for kern, name in arms:
                 med = sorted(res[kern])[2]
                 line += f"  {name} {med:6.2f} us ({nbytes / med / 1e3:6.0f} GB/s)"
             print(line, flush=True)
