@@ -744,7 +744,8 @@ GEMM_4BIT_GEMV_TOKENS = 4
 # (profiles/lab/r02_lib_route.txt, r02_tunableop.txt).  So the first call of such a shape (per device, dtype and
 # statistics format) times both routes on its own operands (one warm call, best of two timed) and keeps the fused
 # kernel only when it wins by more than GEMM_4BIT_ROUTE_MARGIN; otherwise, and during HIP-graph capture, the
-# static rule stands.  The choice is cached for the process.  GEMM_4BIT_ROUTE_TUNING = False: static rule only.
+# static rule stands.  The choice is cached for the process per quarter-octave bucket of the row count
+# (_route_rows_bucket).  GEMM_4BIT_ROUTE_TUNING = False: static rule only.
 GEMM_4BIT_ROUTE_TUNING = True
 GEMM_4BIT_ROUTE_MARGIN = 0.05
 _ROUTES: dict = {}
@@ -753,9 +754,16 @@ _DEQ_WS: dict = {}
 _DEQ_META: dict = {}
 
 
+def _route_rows_bucket(rows: int) -> int:
+    """Row counts share a measured route within quarter-octave buckets (4096..5119 -> 4096, 5120..6143 -> 5120, ...),
+    so variable-length prefill measures at most four buckets per octave and weight shape, not every length."""
+    step = 1 << max(0, rows.bit_length() - 3)
+    return rows // step * step
+
+
 def _route_key(A2: Tensor, state: QuantState, absmax: Optional[Tensor]):
-    return (A2.device.index, A2.shape[0], state.shape[0], state.shape[1], A2.dtype, state.quant_type, state.blocksize,
-            state.nested and absmax is None)
+    return (A2.device.index, _route_rows_bucket(A2.shape[0]), state.shape[0], state.shape[1], A2.dtype,
+            state.quant_type, state.blocksize, state.nested and absmax is None)
 
 
 def gemm_4bit_measured_route(A: Tensor, state: QuantState, absmax: Optional[Tensor] = None) -> Optional[str]:

@@ -130,3 +130,13 @@ def test_golden_fixtures_reproduce(golden):
     rs, cs, _ = ref.colrow_absmax(golden["dq_A"])
     assert np.array_equal(ref.double_quant(golden["dq_A"], rs, cs)[0], golden["dq_row"])
     assert np.array_equal(ref.igemmlt(golden["ig_A"], golden["ig_B"]), golden["ig_C"])
+
+
+def test_route_rows_bucket():
+    """The measured-route cache groups row counts in quarter-octave buckets (host logic, no GPU)."""
+    import python_src_quants.functional as F
+    assert [F._route_rows_bucket(r) for r in (2048, 2559, 2560, 4096, 4500, 5119, 5120, 65536, 70000)] == \
+        [2048, 2048, 2560, 4096, 4096, 4096, 5120, 65536, 65536]
+    for r in range(1, 5000, 7):
+        b = F._route_rows_bucket(r)
+        assert b <= r and r - b < max(1, r // 4 + 1)
