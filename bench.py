@@ -454,7 +454,8 @@ def gemm_kernel_name(m, n, k=K, route=None):
     below, gemm4bit.hip's 256x256 tile kernel when the features are >= 256 and the grid (with split-K) has
     >= 128 workgroups, else the 128x128 one."""
     if m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES and route != "fused":
-        return "hipBLASLt bf16 GEMM (Cijk_*, via torch.matmul) after k_dequantize_4bit_stream<bf16,NF4>"
+        return ("library bf16 GEMM (Cijk_* hipBLASLt kernel via rocBLAS, cgemm_tn_bf16 with the per-shape solution "
+                "search) after k_dequantize_4bit_stream<bf16,NF4>")
     ks = max(1, F.lib.cgemm_4bit_workspace_bytes(ct.c_int32(n), ct.c_int32(m), ct.c_int32(k)) // (4 * m * n))
     tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
     tiles128 = ((m + 127) // 128) * ((n + 127) // 128)
@@ -523,7 +524,7 @@ def main():
     full_out = torch.empty(M, world * shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
     kev = []
 
-    library = gemm_kernel_name(Mc, shard).startswith("hipBLASLt")
+    library = gemm_kernel_name(Mc, shard).startswith("library")
 
     clock = StepClock(args.steps)
 
@@ -559,7 +560,7 @@ def main():
         torch.cuda.synchronize()
     # the route gemm_4bit measured for this shape on its first call (functional.GEMM_4BIT_ROUTE_TUNING)
     kname = gemm_kernel_name(Mc, shard, route=F.gemm_4bit_measured_route(X[:Mc], st))
-    library = kname.startswith("hipBLASLt")
+    library = kname.startswith("library")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

@@ -926,8 +926,14 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
                 events.append(("dequantize", ev[0], ev[1]))
         elif ev:
             ev[1].record()
+        # the library GEMM with the per-shape solution search (gemm_lib.hip: rocBLAS; at the metric shape its standard
+        # algorithm, the same hipBLASLt kernel torch.matmul runs)
+        fn = lib.cgemm_tn_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_tn_fp16
+        rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W), ct.c_int32(K),
+                get_ptr(out), ct.c_int32(N))
         post_call(prev_device)
-        torch.matmul(A2, W.t(), out=out.view(rows, N))
+        if rc:
+            raise RuntimeError(f"bitsandbytes HIP library GEMM error: {lib.cget_last_error_message().decode()}")
         if ev:
             ev[2].record()
             events.append(("gemm", ev[1], ev[2]))

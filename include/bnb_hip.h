@@ -194,6 +194,17 @@ int cigemmlt_row_dequant_ws_fp16(int m, int n, int k, const int8_t* A, const int
 int cigemm_row_i32_ws(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb,
                       int ldc, int32_t* workspace, long long workspace_bytes);
 long long cigemmlt_workspace_bytes(int m, int n, int k);
+/* [additive] the library GEMM of the large-prefill 4-bit path (gemm_lib.hip): C[m, n] = A[m, k] . W[n, k]^T, row-major,
+ * bf16 / fp16 in and out, fp32 accumulation, on rocBLAS with a per-shape solution search (first call of a shape, per
+ * quarter-octave bucket of m; kept only when > 5 % faster than the standard algorithm; none during graph capture).
+ * Replaces the F.linear of ref:autograd/_functions.py:507 after the dequantise.  Returns 0 / 1 (error recorded). */
+int cgemm_tn_bf16(int m, int n, int k, const bnb_bf16* A, int lda, const bnb_bf16* W, int ldw, bnb_bf16* C, int ldc);
+int cgemm_tn_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp16* W, int ldw, bnb_fp16* C, int ldc);
+/* [additive] search switch (0 = standard algorithm only), per-shape budget (ms, > 0 to set), clear != 0 forgets the
+ * cached plans; returns the number of cached plans.  cgemm_tn_plan: the cached plan of a shape (dtype 0 = bf16,
+ * 1 = fp16): 1 = a searched rocBLAS solution, 0 = the standard algorithm, -1 = not searched yet. */
+int cgemm_tn_set_search(int on, double budget_ms, int clear);
+int cgemm_tn_plan(int m, int n, int k, int dtype, int lda, int ldw, int ldc);
 /* [additive, testing] int8 split-K factor: -1 = auto, 1 = never, >= 2 = force where it applies */
 void cigemm_set_splitk(int ks);
 /* [additive, testing] force the int8 GEMM tile kernel: 0 = auto (256x256 when it applies), 128 = 128x128 */

@@ -21,6 +21,19 @@ def _F():
     return F
 
 
+def _lib_matmul(F, X, Wd):
+    """X @ Wd^T through the library GEMM the product's large-prefill route uses (cgemm_tn_*, gemm_lib.hip) with the
+    plan cached for this shape: the reference's F.linear on the dequantised weight."""
+    m, k = X.shape
+    n = Wd.shape[0]
+    out = torch.empty(m, n, device=X.device, dtype=X.dtype)
+    fn = F.lib.cgemm_tn_bf16 if X.dtype == torch.bfloat16 else F.lib.cgemm_tn_fp16
+    F.pre_call(X.device)
+    assert fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(X), ct.c_int32(k), F.get_ptr(Wd), ct.c_int32(k),
+              F.get_ptr(out), ct.c_int32(n)) == 0
+    return out
+
+
 def _close(got, exp, rtol, arel):
     got = np.asarray(got, np.float64)
     exp = np.asarray(exp, np.float64)
@@ -223,7 +236,8 @@ def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
 def test_gemm_4bit_library_path(dev, dtype, qt, monkeypatch):
     """From GEMM_4BIT_DEQUANT_MIN_ROWS x GEMM_4BIT_DEQUANT_MIN_FEATURES gemm_4bit runs the reference's M > 1
     algorithm on the GPU: the HIP dequantise kernel into a workspace, then one library GEMM.  Bit-equal to
-    dequantize_4bit + torch.matmul, within the GEMM tolerance of the oracle, and close to the fused kernel.
+    dequantize_4bit + the library GEMM (cgemm_tn_*), within the GEMM tolerance of the oracle, and close to the fused
+    kernel.
     (The static rule: the measured route is switched off here.)"""
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_ROUTE_TUNING", False)
@@ -234,7 +248,7 @@ def test_gemm_4bit_library_path(dev, dtype, qt, monkeypatch):
     X = torch.randn(M, K, device=dev, dtype=dtype)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type=qt, compress_statistics=True)
     Y = F.gemm_4bit(X, q, st)
-    assert torch.equal(Y, torch.matmul(X, F.dequantize_4bit(q, st).t()))
+    assert torch.equal(Y, _lib_matmul(F, X, F.dequantize_4bit(q, st)))
     absmax = F._absmax_fp32(st).cpu().numpy()
     exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64,
                                     st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
@@ -300,8 +314,10 @@ def test_gemm_4bit_asymmetric_identity(dev):
 
 def test_gemm_4bit_reuse_weight_chunks(dev, monkeypatch):
     """Chunked forward on the library path: chunks after the first reuse the dequantised weight
-    (reuse_weight); the result equals the unchunked call, and a different weight is never reused."""
+    (reuse_weight); the result equals the unchunked call, and a different weight is never reused.  (Standard library
+    algorithm for every row count: the solution search could pick different plans for 2048 and 4096 rows.)"""
     monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
+    _F().lib.cgemm_tn_set_search(0, ct.c_double(0.0), 1)
     F = _F()
     from python_src_quants.parallel import ColumnShardedLinear4bit
     M, N, K = 4096, 1024, 2048
@@ -316,7 +332,8 @@ def test_gemm_4bit_reuse_weight_chunks(dev, monkeypatch):
     W2 = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     q2, st2 = F.quantize_4bit(W2, blocksize=64, quant_type="nf4", compress_statistics=True)
     y2 = F.gemm_4bit(X[:2048], q2, st2, reuse_weight=True)
-    assert torch.equal(y2, torch.matmul(X[:2048], F.dequantize_4bit(q2, st2).t()))
+    assert torch.equal(y2, _lib_matmul(F, X[:2048], F.dequantize_4bit(q2, st2)))
+    F.lib.cgemm_tn_set_search(1, ct.c_double(0.0), 1)
 
 
 def test_gemm_4bit_library_path_two_streams(dev, monkeypatch):
@@ -440,7 +457,7 @@ def test_gemm_4bit_few_tokens_ragged_n(dev, nested, qt, bs, mnk):
 
 def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
     """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 forces the dequantise + library GEMM route for few tokens too (the few-token
-    branch is not taken): the result equals dequantize_4bit + torch.matmul bit for bit."""
+    branch is not taken): the result equals dequantize_4bit + the library GEMM bit for bit."""
     monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1)
@@ -449,7 +466,7 @@ def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
     W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
-    assert torch.equal(F.gemm_4bit(X, q, st), torch.matmul(X, F.dequantize_4bit(q, st).t()))
+    assert torch.equal(F.gemm_4bit(X, q, st), _lib_matmul(F, X, F.dequantize_4bit(q, st)))
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
@@ -615,3 +632,46 @@ def test_fewtoken_whole_k_and_split_k_kernels(dev, dtype, nested, mnk):
     finally:
         F.lib.cgemm_4bit_set_fewtoken_kernel(0)
         F.GEMM_4BIT_GEMV_TOKENS = saved
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mnk", [(2048, 1024, 2048), (300, 520, 640), (4096, 11008, 4096), (1, 64, 64)])
+def test_library_gemm_solution_search(dev, dtype, mnk):
+    """cgemm_tn_* (gemm_lib.hip): C = A . W^T on rocBLAS with the per-shape solution search -- within the bf16/fp16
+    GEMM tolerance of torch.matmul, a plan cached after the first call (>= 0), deterministic on the cached plan, the
+    same bits with the search switched off when the plan is the standard algorithm, and replayable from a HIP graph."""
+    F = _F()
+    m, n, k = mnk
+    torch.manual_seed(m + n)
+    X = torch.randn(m, k, device=dev, dtype=dtype)
+    Wd = (torch.randn(n, k, device=dev) * 0.02).to(dtype)
+    ref_out = torch.matmul(X.float(), Wd.float().t())
+    Y = _lib_matmul(F, X, Wd)
+    err = (Y.float() - ref_out).abs().max().item()
+    assert err <= 1e-2 * ref_out.abs().max().item() + 1e-3, err
+    dt = 0 if dtype == torch.bfloat16 else 1
+    plan = F.lib.cgemm_tn_plan(m, n, k, dt, k, k, n)
+    assert plan >= 0
+    assert torch.equal(_lib_matmul(F, X, Wd), Y)
+    if plan == 0:
+        F.lib.cgemm_tn_set_search(0, ct.c_double(0.0), 0)
+        try:
+            assert torch.equal(_lib_matmul(F, X, Wd), Y)
+        finally:
+            F.lib.cgemm_tn_set_search(1, ct.c_double(0.0), 0)
+    # HIP-graph capture of the planned call (the plan and rocBLAS's workspace exist from the calls above), replayed
+    X2 = torch.randn(m, k, device=dev, dtype=dtype)
+    Y2 = torch.empty(m, n, device=dev, dtype=dtype)
+    fn = F.lib.cgemm_tn_bf16 if dtype == torch.bfloat16 else F.lib.cgemm_tn_fp16
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            F.pre_call(X2.device)
+            fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(X2), ct.c_int32(k), F.get_ptr(Wd), ct.c_int32(k),
+               F.get_ptr(Y2), ct.c_int32(n))
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(Y2, _lib_matmul(F, X2, Wd))

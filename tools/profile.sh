@@ -13,10 +13,10 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/fetc
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/write -- python3 bench.py --no-extras --no-cpu --steps 3 --warmup 1 > /dev/null 2> $OUT/write.err || exit 3
 # MFMA utilisation and the clock held under load (counters only; durations come from the trace pass above)
 timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES -T --output-format csv -d $OUT/mfma -- python3 bench.py --no-extras --no-cpu --steps 3 --warmup 1 > /dev/null 2> $OUT/mfma.err || exit 6
-# the kernel that carries the metric's flops at 4096 x 4096 x 11008 (bench.gemm_kernel_name): the hipBLASLt
+# the kernel that carries the metric's flops at 4096 x 4096 x 11008 (bench.gemm_kernel_name): the library
 # GEMM (Cijk_*) after the dequantise kernel, or the fused k_gemm_4bit_256 when routed there
 LABEL=$(python3 -c "import bench; print(bench.gemm_kernel_name(4096, 4096))" 2>/dev/null | tail -1)
-case "$LABEL" in hipBLASLt*) MATCH="Cijk" ;; *) MATCH="k_gemm_4bit_256" ;; esac
+case "$LABEL" in library*) MATCH="Cijk" ;; *) MATCH="k_gemm_4bit_256" ;; esac
 python3 tools/pmc_traffic.py $OUT/fetch $OUT/write "$MATCH" $OUT/pmc_traffic.json 4096 4096 11008 "$LABEL" $OUT/mfma $OUT/trace || exit 4
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/${TAG}_kernel_stats.csv \;
 find $OUT/trace_extras -name "*kernel_stats.csv" -exec cp {} $OUT/${TAG}_kernel_stats_extras.csv \;
