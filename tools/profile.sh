@@ -16,7 +16,16 @@ timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BU
 # the kernel that carries the metric's flops at 4096 x 4096 x 11008 (bench.gemm_kernel_name): the library
 # GEMM (Cijk_*) after the dequantise kernel, or the fused k_gemm_4bit_256 when routed there
 LABEL=$(python3 -c "import bench; print(bench.gemm_kernel_name(4096, 4096))" 2>/dev/null | tail -1)
-case "$LABEL" in library*) MATCH="Cijk" ;; *) MATCH="k_gemm_4bit_256" ;; esac
+# library route: the exact name of the most-launched Cijk kernel of the metric trace (the per-shape solution search
+# launches other Cijk kernels a few times each on the first call; a substring match would count them too)
+case "$LABEL" in
+  library*) MATCH=$(python3 -c "
+import csv, glob, sys
+rows = [r for p in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True) for r in csv.DictReader(open(p))
+        if 'Cijk' in r['Name']]
+print(max(rows, key=lambda r: int(r['Calls']))['Name'] if rows else 'Cijk')" $OUT/trace) ;;
+  *) MATCH="k_gemm_4bit_256" ;;
+esac
 python3 tools/pmc_traffic.py $OUT/fetch $OUT/write "$MATCH" $OUT/pmc_traffic.json 4096 4096 11008 "$LABEL" $OUT/mfma $OUT/trace || exit 4
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/${TAG}_kernel_stats.csv \;
 find $OUT/trace_extras -name "*kernel_stats.csv" -exec cp {} $OUT/${TAG}_kernel_stats_extras.csv \;
