@@ -450,12 +450,15 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
 
 def gemm_kernel_name(m, n, k=K, route=None):
     """Which kernel carries gemm_4bit's flops for m tokens x n features: from GEMM_4BIT_DEQUANT_MIN_ROWS
-    tokens the library GEMM after the dequantise kernel (unless the measured route, `route`, is "fused");
+    tokens the library GEMM after the dequantise kernel (torch's hipBLASLt pick, or with route "library_tn" the
+    rocBLAS-searched one; unless the measured route, `route`, is "fused");
     below, gemm4bit.hip's 256x256 tile kernel when the features are >= 256 and the grid (with split-K) has
     >= 128 workgroups, else the 128x128 one."""
     if m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES and route != "fused":
-        return ("library bf16 GEMM (Cijk_* hipBLASLt kernel via rocBLAS, cgemm_tn_bf16 with the per-shape solution "
-                "search) after k_dequantize_4bit_stream<bf16,NF4>")
+        if route == "library_tn":
+            return ("library bf16 GEMM (Cijk_*, rocBLAS solution searched per shape, cgemm_tn_bf16) after "
+                    "k_dequantize_4bit_stream<bf16,NF4>")
+        return "library bf16 GEMM (Cijk_* hipBLASLt, via torch.matmul) after k_dequantize_4bit_stream<bf16,NF4>"
     ks = max(1, F.lib.cgemm_4bit_workspace_bytes(ct.c_int32(n), ct.c_int32(m), ct.c_int32(k)) // (4 * m * n))
     tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
     tiles128 = ((m + 127) // 128) * ((n + 127) // 128)

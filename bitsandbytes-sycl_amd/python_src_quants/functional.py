@@ -739,13 +739,15 @@ GEMM_4BIT_GEMV_TOKENS = 4
 
 # Measured route for prefill shapes.  Where the static rule picks the dequantise + library pair (rows >=
 # GEMM_4BIT_DEQUANT_MIN_ROWS), the library's own solution choice can be far off for some shapes: torch's default
-# hipBLASLt heuristic runs 4096 x 11008 x 4096 (rows x out x in: the gate/up projection at 4096 tokens) at 0.87
-# PFLOP/s, where the fused kernel reaches 1.06 and the library itself 1.48 with a tuned solution
-# (profiles/lab/r02_lib_route.txt, r02_tunableop.txt).  So the first call of such a shape (per device, dtype and
-# statistics format) times both routes on its own operands (one warm call, best of two timed) and keeps the fused
-# kernel only when it wins by more than GEMM_4BIT_ROUTE_MARGIN; otherwise, and during HIP-graph capture, the
-# static rule stands.  The choice is cached for the process per quarter-octave bucket of the row count
-# (_route_rows_bucket).  GEMM_4BIT_ROUTE_TUNING = False: static rule only.
+# hipBLASLt heuristic runs 4096 x 11008 x 4096 (rows x out x in: the gate/up projection at 4096 tokens) at 0.9
+# PFLOP/s, where the fused kernel reaches 1.06 and a searched rocBLAS solution 1.45 (profiles/lab/r02_lib_route.txt,
+# r02_rocblas_solutions.txt).  So the first call of such a shape (per device, dtype and statistics format) times three
+# routes on its own operands (one warm call, best of two timed): "library" (dequantise + torch.matmul, torch's
+# hipBLASLt heuristic), "library_tn" (dequantise + cgemm_tn_*, rocBLAS with the per-shape solution search of
+# gemm_lib.hip) and "fused" (the hand-written kernel), and leaves "library" only for a route faster by more than
+# GEMM_4BIT_ROUTE_MARGIN; during HIP-graph capture nothing is timed and the static rule stands.  The choice is cached
+# for the process per quarter-octave bucket of the row count (_route_rows_bucket).  GEMM_4BIT_ROUTE_TUNING = False:
+# static rule only.
 GEMM_4BIT_ROUTE_TUNING = True
 GEMM_4BIT_ROUTE_MARGIN = 0.05
 _ROUTES: dict = {}
@@ -767,21 +769,21 @@ def _route_key(A2: Tensor, state: QuantState, absmax: Optional[Tensor]):
 
 
 def gemm_4bit_measured_route(A: Tensor, state: QuantState, absmax: Optional[Tensor] = None) -> Optional[str]:
-    """The measured route ("library" / "fused") cached for A's rows against this weight, or None when the shape
-    has not been measured (the static rule applies)."""
+    """The measured route ("library" / "library_tn" / "fused") cached for A's rows against this weight, or None when
+    the shape has not been measured (the static rule applies)."""
     return _ROUTES.get(_route_key(A.reshape(-1, state.shape[1]), state, absmax))
 
 
-def _tuned_library_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor]) -> bool:
-    """True: keep the dequantise + library pair for this shape; False: the fused kernel measured faster."""
+def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor]) -> str:
+    """The measured route of a library-side prefill shape: "library", "library_tn" or "fused" (see above)."""
     key = _route_key(A2, state, absmax)
     route = _ROUTES.get(key)
     if route is not None:
-        return route == "library"
+        return route
     if torch.cuda.is_current_stream_capturing():
-        return True
+        return "library"
     times = {}
-    for name in ("library", "fused"):
+    for name in ("library", "library_tn", "fused"):
         gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
         best = None
         for _ in range(2):
@@ -793,9 +795,10 @@ def _tuned_library_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor,
             t = s.elapsed_time(e)
             best = t if best is None else min(best, t)
         times[name] = best
-    route = "fused" if times["fused"] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times["library"] else "library"
+    fastest = min(times, key=times.get)
+    route = fastest if times[fastest] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times["library"] else "library"
     _ROUTES[key] = route
-    return route == "library"
+    return route
 
 
 def _dequant_workspace(device, dtype, numel: int) -> Tensor:
@@ -855,7 +858,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     the caller runs several row chunks of one product against the same, unmodified weight (the chunked
     sharded forward); on the library path the workspace still holding this weight's dequantisation
     from the previous call is used as is.  Prefill shapes on the library side of the static rule take the
-    measured route (GEMM_4BIT_ROUTE_TUNING); _route ("library" / "fused") forces one (internal)."""
+    measured route (GEMM_4BIT_ROUTE_TUNING); _route ("library" / "library_tn" / "fused") forces one (internal)."""
     if not gemm_4bit_supported(A, state):
         raise ValueError("gemm_4bit: needs bf16/fp16 activations and in_features % 64 == 0")
     N, K = state.shape[0], state.shape[1]
@@ -868,10 +871,12 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
+    route = "library" if library else "fused"
     if _route is not None:
-        library = _route == "library"
+        route = _route
     elif library and rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and GEMM_4BIT_ROUTE_TUNING:
-        library = _tuned_library_route(A2, Bc, state, out.view(rows, N), absmax)
+        route = _tuned_route(A2, Bc, state, out.view(rows, N), absmax)
+    library = route in ("library", "library_tn")
     if not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events):
         return out.view(*A.shape[:-1], N)
     if (absmax is None and not library and rows <= GEMM_4BIT_FEW_TOKENS and _nested_stats_in_kernel_ok(state)):
@@ -926,14 +931,17 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
                 events.append(("dequantize", ev[0], ev[1]))
         elif ev:
             ev[1].record()
-        # the library GEMM with the per-shape solution search (gemm_lib.hip: rocBLAS; at the metric shape its standard
-        # algorithm, the same hipBLASLt kernel torch.matmul runs)
-        fn = lib.cgemm_tn_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_tn_fp16
-        rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W), ct.c_int32(K),
-                get_ptr(out), ct.c_int32(N))
-        post_call(prev_device)
-        if rc:
-            raise RuntimeError(f"bitsandbytes HIP library GEMM error: {lib.cget_last_error_message().decode()}")
+        if route == "library_tn":
+            # the library GEMM with the per-shape solution search (gemm_lib.hip, rocBLAS)
+            fn = lib.cgemm_tn_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_tn_fp16
+            rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W),
+                    ct.c_int32(K), get_ptr(out), ct.c_int32(N))
+            post_call(prev_device)
+            if rc:
+                raise RuntimeError(f"bitsandbytes HIP library GEMM error: {lib.cget_last_error_message().decode()}")
+        else:
+            post_call(prev_device)
+            torch.matmul(A2, W.t(), out=out.view(rows, N))
         if ev:
             ev[2].record()
             events.append(("gemm", ev[1], ev[2]))

@@ -236,8 +236,8 @@ def test_gemm_4bit_split_k_vs_oracle(dev, dtype, mnk, ks):
 def test_gemm_4bit_library_path(dev, dtype, qt, monkeypatch):
     """From GEMM_4BIT_DEQUANT_MIN_ROWS x GEMM_4BIT_DEQUANT_MIN_FEATURES gemm_4bit runs the reference's M > 1
     algorithm on the GPU: the HIP dequantise kernel into a workspace, then one library GEMM.  Bit-equal to
-    dequantize_4bit + the library GEMM (cgemm_tn_*), within the GEMM tolerance of the oracle, and close to the fused
-    kernel.
+    dequantize_4bit + torch.matmul (the static rule's library GEMM), within the GEMM tolerance of the oracle, and close
+    to the fused kernel.
     (The static rule: the measured route is switched off here.)"""
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_ROUTE_TUNING", False)
@@ -248,7 +248,7 @@ def test_gemm_4bit_library_path(dev, dtype, qt, monkeypatch):
     X = torch.randn(M, K, device=dev, dtype=dtype)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type=qt, compress_statistics=True)
     Y = F.gemm_4bit(X, q, st)
-    assert torch.equal(Y, _lib_matmul(F, X, F.dequantize_4bit(q, st)))
+    assert torch.equal(Y, torch.matmul(X, F.dequantize_4bit(q, st).t()))
     absmax = F._absmax_fp32(st).cpu().numpy()
     exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64,
                                     st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
@@ -314,10 +314,8 @@ def test_gemm_4bit_asymmetric_identity(dev):
 
 def test_gemm_4bit_reuse_weight_chunks(dev, monkeypatch):
     """Chunked forward on the library path: chunks after the first reuse the dequantised weight
-    (reuse_weight); the result equals the unchunked call, and a different weight is never reused.  (Standard library
-    algorithm for every row count: the solution search could pick different plans for 2048 and 4096 rows.)"""
+    (reuse_weight); the result equals the unchunked call, and a different weight is never reused."""
     monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
-    _F().lib.cgemm_tn_set_search(0, ct.c_double(0.0), 1)
     F = _F()
     from python_src_quants.parallel import ColumnShardedLinear4bit
     M, N, K = 4096, 1024, 2048
@@ -332,8 +330,7 @@ def test_gemm_4bit_reuse_weight_chunks(dev, monkeypatch):
     W2 = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     q2, st2 = F.quantize_4bit(W2, blocksize=64, quant_type="nf4", compress_statistics=True)
     y2 = F.gemm_4bit(X[:2048], q2, st2, reuse_weight=True)
-    assert torch.equal(y2, _lib_matmul(F, X[:2048], F.dequantize_4bit(q2, st2)))
-    F.lib.cgemm_tn_set_search(1, ct.c_double(0.0), 1)
+    assert torch.equal(y2, torch.matmul(X[:2048], F.dequantize_4bit(q2, st2).t()))
 
 
 def test_gemm_4bit_library_path_two_streams(dev, monkeypatch):
@@ -457,7 +454,7 @@ def test_gemm_4bit_few_tokens_ragged_n(dev, nested, qt, bs, mnk):
 
 def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
     """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 forces the dequantise + library GEMM route for few tokens too (the few-token
-    branch is not taken): the result equals dequantize_4bit + the library GEMM bit for bit."""
+    branch is not taken): the result equals dequantize_4bit + torch.matmul bit for bit."""
     monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1)
@@ -466,7 +463,7 @@ def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
     W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
-    assert torch.equal(F.gemm_4bit(X, q, st), _lib_matmul(F, X, F.dequantize_4bit(q, st)))
+    assert torch.equal(F.gemm_4bit(X, q, st), torch.matmul(X, F.dequantize_4bit(q, st).t()))
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
