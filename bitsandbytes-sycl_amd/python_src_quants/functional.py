@@ -8,6 +8,7 @@ there is no CPU/torch fallback for them.
 from __future__ import annotations
 
 import ctypes as ct
+import os
 import threading
 import weakref
 from functools import reduce
@@ -746,9 +747,10 @@ GEMM_4BIT_GEMV_TOKENS = 4
 # hipBLASLt heuristic), "library_tn" (dequantise + cgemm_tn_*, rocBLAS with the per-shape solution search of
 # gemm_lib.hip) and "fused" (the hand-written kernel), and leaves "library" only for a route faster by more than
 # GEMM_4BIT_ROUTE_MARGIN; during HIP-graph capture nothing is timed and the static rule stands.  The choice is cached
-# for the process per quarter-octave bucket of the row count (_route_rows_bucket).  GEMM_4BIT_ROUTE_TUNING = False:
-# static rule only.
-GEMM_4BIT_ROUTE_TUNING = True
+# for the process per quarter-octave bucket of the row count (_route_rows_bucket).  The first call of a bucket costs
+# about a second (the rocBLAS solution search included).  GEMM_4BIT_ROUTE_TUNING = False (or BNB_ROUTE_TUNING=0 in
+# the environment): static rule only.
+GEMM_4BIT_ROUTE_TUNING = os.environ.get("BNB_ROUTE_TUNING", "1") != "0"
 GEMM_4BIT_ROUTE_MARGIN = 0.05
 _ROUTES: dict = {}
 
