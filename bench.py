@@ -555,6 +555,10 @@ def main():
     # clock ramp: MI355X takes ~0.1-0.3 s of sustained MFMA load to reach its steady clock; run the
     # step untimed for --prewarm-ms before the W counted warmup steps (the timed region is unchanged)
     # (GEMM only: a time-based loop must not contain a collective, ranks could disagree on its count)
+    # the first call of the shape measures its route (functional.GEMM_4BIT_ROUTE_TUNING; about a second with the
+    # library solution search): done before the clock-ramp period starts, so the ramp is not spent on it
+    F.gemm_4bit(X[:Mc], q, st, out=Y[:Mc], absmax=None if library else F._absmax_fp32(st))
+    torch.cuda.synchronize()
     t_end = time.perf_counter() + args.prewarm_ms / 1e3
     while time.perf_counter() < t_end:
         am = None if library else F._absmax_fp32(st)
