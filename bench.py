@@ -454,7 +454,8 @@ def gemm_kernel_name(m, n, k=K, route=None):
     rocBLAS-searched one; unless the measured route, `route`, is "fused");
     below, gemm4bit.hip's 256x256 tile kernel when the features are >= 256 and the grid (with split-K) has
     >= 128 workgroups, else the 128x128 one."""
-    if m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES and route != "fused":
+    static_library = m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES
+    if route in ("library", "library_tn") or (route is None and static_library):
         if route == "library_tn":
             return ("library bf16 GEMM (Cijk_*, rocBLAS solution searched per shape, cgemm_tn_bf16) after "
                     "k_dequantize_4bit_stream<bf16,NF4>")

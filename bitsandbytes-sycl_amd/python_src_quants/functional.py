@@ -738,15 +738,16 @@ GEMM_4BIT_WIDE_MAX_ROWS = 256
 # once and dotted with each row, whole K per workgroup, one launch, rows bit-identical to gemv_4bit on each row).
 GEMM_4BIT_GEMV_TOKENS = 4
 
-# Measured route for prefill shapes.  Where the static rule picks the dequantise + library pair (rows >=
-# GEMM_4BIT_DEQUANT_MIN_ROWS), the library's own solution choice can be far off for some shapes: torch's default
-# hipBLASLt heuristic runs 4096 x 11008 x 4096 (rows x out x in: the gate/up projection at 4096 tokens) at 0.9
-# PFLOP/s, where the fused kernel reaches 1.06 and a searched rocBLAS solution 1.45 (profiles/lab/r02_lib_route.txt,
-# r02_rocblas_solutions.txt).  So the first call of such a shape (per device, dtype and statistics format) times three
-# routes on its own operands (one warm call, best of two timed): "library" (dequantise + torch.matmul, torch's
-# hipBLASLt heuristic), "library_tn" (dequantise + cgemm_tn_*, rocBLAS with the per-shape solution search of
-# gemm_lib.hip) and "fused" (the hand-written kernel), and leaves "library" only for a route faster by more than
-# GEMM_4BIT_ROUTE_MARGIN; during HIP-graph capture nothing is timed and the static rule stands.  The choice is cached
+# Measured route for prefill shapes (more than GEMM_4BIT_FEW_TOKENS rows).  The static rule above is a coarse map and
+# the libraries' own solution choice can be far off: torch's default hipBLASLt heuristic runs 4096 x 11008 x 4096
+# (rows x out x in: the gate/up projection at 4096 tokens) at 0.9 PFLOP/s, where the fused kernel reaches 1.06 and a
+# searched rocBLAS solution 1.45; at 1536 rows the fused kernel's 258 tiles take two passes over 256 CUs and the pair
+# is 1.5-1.7x faster (profiles/lab/r02_lib_route.txt, r02_rocblas_solutions.txt, r02_mid_rows_route.txt).  So the
+# first call of a shape (per device, dtype and statistics format) times three routes on its own operands (one warm
+# call, best of two timed): "library" (dequantise + torch.matmul, torch's hipBLASLt heuristic), "library_tn"
+# (dequantise + cgemm_tn_*, rocBLAS with the per-shape solution search of gemm_lib.hip) and "fused" (the hand-written
+# kernel), and leaves the static rule's route only for one faster by more than GEMM_4BIT_ROUTE_MARGIN; during
+# HIP-graph capture nothing is timed and the static rule stands.  The choice is cached
 # for the process per quarter-octave bucket of the row count (_route_rows_bucket).  The first call of a bucket costs
 # about a second (the rocBLAS solution search included).  GEMM_4BIT_ROUTE_TUNING = False (or BNB_ROUTE_TUNING=0 in
 # the environment): static rule only.
@@ -776,14 +777,16 @@ def gemm_4bit_measured_route(A: Tensor, state: QuantState, absmax: Optional[Tens
     return _ROUTES.get(_route_key(A.reshape(-1, state.shape[1]), state, absmax))
 
 
-def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor]) -> str:
-    """The measured route of a library-side prefill shape: "library", "library_tn" or "fused" (see above)."""
+def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor],
+                 default: str) -> str:
+    """The measured route of a prefill shape: "library", "library_tn" or "fused" (see above); `default` is the static
+    rule's route, kept unless another is faster by more than GEMM_4BIT_ROUTE_MARGIN."""
     key = _route_key(A2, state, absmax)
     route = _ROUTES.get(key)
     if route is not None:
         return route
     if torch.cuda.is_current_stream_capturing():
-        return "library"
+        return default
     times = {}
     for name in ("library", "library_tn", "fused"):
         gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
@@ -798,7 +801,7 @@ def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax:
             best = t if best is None else min(best, t)
         times[name] = best
     fastest = min(times, key=times.get)
-    route = fastest if times[fastest] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times["library"] else "library"
+    route = fastest if times[fastest] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times[default] else default
     _ROUTES[key] = route
     return route
 
@@ -876,8 +879,8 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     route = "library" if library else "fused"
     if _route is not None:
         route = _route
-    elif library and rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and GEMM_4BIT_ROUTE_TUNING:
-        route = _tuned_route(A2, Bc, state, out.view(rows, N), absmax)
+    elif GEMM_4BIT_ROUTE_TUNING and rows > GEMM_4BIT_FEW_TOKENS:
+        route = _tuned_route(A2, Bc, state, out.view(rows, N), absmax, route)
     library = route in ("library", "library_tn")
     if not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events):
         return out.view(*A.shape[:-1], N)

@@ -3,6 +3,7 @@ NF4 bs 64, nested statistics), interleaved over rounds:
   fused    : k_gemm_4bit_256 (the hand-written fused kernel, forced)
   lt       : our dequantise + torch.matmul on hipBLASLt (torch's default BLAS on ROCm)
   rocblas  : our dequantise + torch.matmul on rocBLAS (torch.backends.cuda.preferred_blas_library("cublas"))
+  searched : our dequantise + cgemm_tn (rocBLAS with the per-shape solution search of gemm_lib.hip)
 Usage: python tools/lib_route_probe.py [MxNxK ...]"""
 import os
 import sys
@@ -52,7 +53,9 @@ def main():
                 finally:
                     torch.backends.cuda.preferred_blas_library("cublaslt")
             return go
-        arms = {"fused": fused, "lt": lib("cublaslt"), "rocblas": lib("cublas")}
+        def tn():
+            F.gemm_4bit(X, q, st, out=Y, _route="library_tn")
+        arms = {"fused": fused, "lt": lib("cublaslt"), "rocblas": lib("cublas"), "searched": tn}
         t_end = time.perf_counter() + 1.0
         while time.perf_counter() < t_end:
             fused()
