@@ -288,9 +288,10 @@ k_igemm_splitk_reduce(const int32_t* __restrict__ ws, int ksplit, int M, int N, 
 static int g_igemm_splitk = -1;   // < 0: auto; 1 = never split; >= 2: force that factor where it applies (tests)
 
 // Split-K factor for a row-major 256-tile problem: enough workgroups for the 256 CUs when the output has fewer
-// than ~200 tiles, with at least 8 k-tiles (1024 k) per split, at most 16 splits.
+// than ~200 tiles, with at least 8 k-tiles (1024 k) per split -- 2 below 256 rows (few-token forwards, where the
+// weight stream is the work) -- at most 16 splits.
 int igemm_splitk_factor(int m, int n, int k) {
-  if (k % J_BK != 0 || m < 256 || n < 256) return 1;
+  if (k % J_BK != 0 || m < 1 || n < 256) return 1;
   const long long tiles = (long long)((m + J_BM - 1) / J_BM) * ((n + J_BN - 1) / J_BN);
   int ks;
   if (g_igemm_splitk >= 1) {
@@ -299,7 +300,7 @@ int igemm_splitk_factor(int m, int n, int k) {
     if (tiles >= 200) return 1;
     ks = (int)((256 + tiles / 2) / tiles);
   }
-  ks = std::min(ks, std::max(1, (k / J_BK) / 8));
+  ks = std::min(ks, std::max(1, (k / J_BK) / (m < 256 ? 2 : 8)));
   return std::max(1, std::min(ks, 16));
 }
 
@@ -315,7 +316,9 @@ bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, voi
   if constexpr (AF == TURING) {
     return false;                                                  // A in 4-byte runs: register-staged kernel
   } else {
-    if (k % J_BK != 0 || m < 256 || n < 256) return false;
+    // below 256 rows only the split-K form (row-major operands, a workspace), which fills the chip from the
+    // weight side; otherwise the 128-tile kernel
+    if (k % J_BK != 0 || n < 256 || m < 1) return false;
     if ((AF == ROW && lda % 16) || (BF == ROW && ldb % 16) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return false;
     if (BF == TURING && (ldb % 256 || ldb < 32LL * n || (long long)(k / 32) * ldb >= (1LL << 32))) return false;
     const long long tiles = (long long)((m + J_BM - 1) / J_BM) * ((n + J_BN - 1) / J_BN);
@@ -333,6 +336,7 @@ bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, voi
         return true;
       }
     }
+    if (m < 256) return false;
     hipLaunchKernelGGL((k_igemm_256<AF, BF, EPI>), dim3((unsigned)tiles), dim3(J_THREADS), 0, current_stream(), m, n,
                        k, A, B, C, row_scale, lda, ldb, ldc, rowStats, colStats, bias, nullptr, 1);
     return true;

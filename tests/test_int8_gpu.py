@@ -246,7 +246,7 @@ def test_igemmlt_turing_abi_all_epilogues(dev, mnk):
 
 
 @pytest.mark.parametrize("mnk", [(4096, 512, 11008), (2048, 512, 11008), (2048, 1024, 4096), (4096, 2048, 11008),
-                                 (300, 258, 2048), (513, 777, 3072)])
+                                 (300, 258, 2048), (513, 777, 3072), (8, 4096, 4096), (33, 1030, 2048), (1, 256, 1024)])
 def test_igemm_split_k_exact(dev, mnk):
     """Split-K over a workspace for small 256-tile grids (the column shards of the multi-GPU step): the int32
     partials are summed exactly, so the int32 result equals the exact product (fp64 GPU matmul) and the fused
@@ -274,6 +274,6 @@ def test_igemm_split_k_exact(dev, mnk):
         assert torch.equal(o, exp)
     for o in outs16[1:]:
         assert torch.equal(o.view(torch.int16), outs16[0].view(torch.int16))
-    if m >= 256 and n >= 256 and k % 128 == 0:
+    if n >= 256 and k % 128 == 0 and k >= 2 * 128 * (2 if m < 256 else 8):
         tiles = ((m + 255) // 256) * ((n + 255) // 256)
         assert (F.lib.cigemmlt_workspace_bytes(m, n, k) > 0) == (tiles < 200)

@@ -1,7 +1,7 @@
 """A/B (GPU): the fused igemmlt + dequant on the column shards of the multi-GPU INT8 step (tokens x N/g x K,
 metric shape 4096 x 4096 x 11008, g = 1/2/4/8, and the 2-chunk halves the overlapped step runs), with the int8
 split-K (auto) against the unsplit 256-tile kernel (cigemm_set_splitk(1)); interleaved rounds, medians.
-Usage: python tools/int8_split_ab.py"""
+Usage: [INT8_ROWS=4096,2048 INT8_COLS=4096,2048,1024,512] python tools/int8_split_ab.py"""
 import os
 import sys
 
@@ -27,10 +27,10 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     K = 11008
-    for m in (4096, 2048):
+    for m in [int(v) for v in os.environ.get("INT8_ROWS", "4096,2048").split(",")]:
         A = torch.randint(-127, 128, (m, K), device=dev, dtype=torch.int8, generator=g)
         rs = torch.rand(m, device=dev, generator=g) + 0.5
-        for n in (4096, 2048, 1024, 512):
+        for n in [int(v) for v in os.environ.get("INT8_COLS", "4096,2048,1024,512").split(",")]:
             B = torch.randint(-127, 128, (n, K), device=dev, dtype=torch.int8, generator=g)
             cs = torch.rand(n, device=dev, generator=g) + 0.5
             out = torch.empty(m, n, device=dev, dtype=torch.float16)
