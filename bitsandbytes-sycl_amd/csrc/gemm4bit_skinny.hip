@@ -25,6 +25,7 @@
 #include "gemm_common.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace bnb {
 #ifndef LUTC_DEF
@@ -36,7 +37,8 @@ namespace bnb {
 #define SK_STAMP(i)
 #endif
 
-constexpr int SK_THREADS = 256, SK_ROWS = 64, SK_LUTC = LUTC_DEF, SK_MAX_TOKENS = 64;
+[[maybe_unused]] constexpr int SK_THREADS = 256, SK_ROWS = 64;  // base form (labs)
+constexpr int SK_LUTC = LUTC_DEF, SK_MAX_TOKENS = 64;
 
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -51,32 +53,37 @@ template <> __device__ __forceinline__ uint32_t sk_cvt2v<fp16_t>(f32x2_t v) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_t));
 }
 
-// ABL (design lab only, tools/skinny_lab.hip): 1 = no weight loads, 2 = no activation DMA, 4 = no MFMA
-template <typename T, int MT, int NB, bool NESTED, int ABL = 0>
-__global__ void __launch_bounds__(SK_THREADS, 2)
+// ABL (design lab only, tools/skinny_lab.hip): 1 = no weight loads, 2 = no activation DMA, 4 = no MFMA.
+// W = waves per workgroup (16 W weight rows share one LDS copy of the token rows): 4, or 8 (half the activation
+// DMA per weight row, one workgroup per CU).
+template <typename T, int MT, int NB, bool NESTED, int ABL = 0, int W = 4>
+__global__ void __launch_bounds__(64 * W, W == 4 ? 2 : 1)
 k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
                    SkStats st, const float* __restrict__ code, float* __restrict__ ws, T* __restrict__ out, int ldc,
                    int nsplit) {
   constexpr int MP = 16 * MT;                    // token rows held (padded to the MFMA width)
   constexpr int XBLK = MP * 256;                 // LDS bytes of one 128-k block of all tokens
-  constexpr int XP = NB * MT;                    // 1-KiB activation DMA pieces per wave (4 waves)
+  constexpr int THREADS = 64 * W, ROWS = 16 * W;
+  constexpr int XP = NB * MT * 4 / W;            // 1-KiB activation DMA pieces per wave
+  static_assert((NB * MT * 4) % W == 0, "whole DMA pieces per wave");
   __shared__ __attribute__((aligned(16))) uint8_t xs[(NB + 1) * XBLK];   // + one zero block
   __shared__ float2 lut[256 * SK_LUTC];
   __shared__ float c2s[NESTED ? 256 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rb = blockIdx.x / nsplit, split = blockIdx.x - rb * nsplit;
   const int r = lane & 15, c = lane >> 4;
-  const int rowc = min(rb * SK_ROWS + 16 * wave + r, N - 1);
+  const int rowc = min(rb * ROWS + 16 * wave + r, N - 1);
   const int kb0 = split * NB;                                  // first 128-k block of this split
   const int nb = min(NB, (K >> 7) - kb0);                      // >= 1 by construction
   SK_STAMP(0);
 
   // (1a) table values and statistics first: their consumers must not wait on the weight loads below
   // (the VMEM counter retires in order)
-  const float code_hi = code[tid >> 4], code_lo = code[tid & 15];
+  const int te = tid & 255;                                    // table entry of this thread (tid < 256 stores)
+  const float code_hi = code[te >> 4], code_lo = code[te & 15];
   float off = 0.0f, c2v = 0.0f;
   if constexpr (NESTED) {
-    c2v = st.code2[tid];
+    c2v = st.code2[te];
     off = *st.offset;
   }
   const long long abase = 2LL * ldb * rowc + 32 * c + 128LL * kb0;   // element index of (row, k)
@@ -97,7 +104,7 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
   // row 4 (p % 4MT) + (l >> 4), LDS slot l & 15 holding source slot (l & 15) ^ (row & 15)
 #pragma unroll
   for (int i = 0; i < ((ABL & 2) ? 0 : XP); ++i) {
-    const int p = wave + 4 * i;
+    const int p = wave + W * i;
     const int blk = p / (4 * MT), t = 4 * (p % (4 * MT)) + (lane >> 4);
     const int gslot = (lane & 15) ^ (t & 15);
     glds16(A + (long long)min(t, M - 1) * lda + 128LL * (kb0 + min(blk, nb - 1)) + 8 * gslot,
@@ -122,14 +129,13 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
     }
   }
   // (2) table (+ nested code map) while the loads fly: entry tid, copies 0..SK_LUTC-1
-  static_assert(SK_THREADS == 256, "one table entry per thread");
+  if (tid < 256) {
 #pragma unroll
-  for (int j = 0; j < SK_LUTC; ++j) lut[tid * SK_LUTC + j] = make_float2(code_hi, code_lo);
-  if constexpr (NESTED) c2s[tid] = c2v;
+    for (int j = 0; j < SK_LUTC; ++j) lut[tid * SK_LUTC + j] = make_float2(code_hi, code_lo);
+    if constexpr (NESTED) c2s[tid] = c2v;
+  }
   // a zero activation block: blocks past a short last split multiply it (exact zeros, no branch)
-#pragma unroll
-  for (int i = 0; i < XBLK / (16 * SK_THREADS); ++i)
-    *reinterpret_cast<uint4*>(xs + NB * XBLK + 16 * (tid + SK_THREADS * i)) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < XBLK / 16; i += THREADS) *reinterpret_cast<uint4*>(xs + NB * XBLK + 16 * i) = make_uint4(0, 0, 0, 0);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NB) : "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
@@ -189,7 +195,7 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
 
   SK_STAMP(2);
   // D[i]: weight row 4c + i of the wave's 16, token 16g + r -> 4 consecutive features per lane
-  const int row0 = rb * SK_ROWS + 16 * wave + 4 * c;
+  const int row0 = rb * ROWS + 16 * wave + 4 * c;
 #pragma unroll
   for (int g = 0; g < MT; ++g) {
     const int t = 16 * g + r;
@@ -267,15 +273,42 @@ bool skinny_applicable(int m, int n, int k, int lda, int ldb, int blocksize, con
          ((uintptr_t)B & 15) == 0;
 }
 
-int skinny_splits(int n, int k) {
-  const int mt = skinny_tiles(n);
-  const int nbw = mt == 1 ? skinny_nb<1>() : (mt == 2 ? skinny_nb<2>() : skinny_nb<4>());
-  return (k / 128 + nbw - 1) / nbw;
+// Geometry (profiles/lab/r02_skinny_waves.txt).  The base form is 4 waves (64 weight rows) per workgroup with the NB
+// above.  At 33..64 rows a second form, 8 waves (128 weight rows sharing one LDS copy of the token rows) with twice the
+// blocks per split, halves the splits and so the fp32 partials the reduce re-reads: 4096 x 11008 at 64 rows 32.9 ->
+// 28.0 us, 4096 x 4096 19.3 -> 17.4 us.  It has a quarter of the workgroups, so it loses when its last round of
+// workgroups is mostly empty (11008 x 4096: 516 workgroups on 256 CUs, 30.2 -> 36.8 us at 48 rows); it is taken when
+// that round is at least 70 % full.  At 1..32 rows the 8-wave forms lost everywhere (same NB: +1..3 us; 2 x NB: +5..14 us).
+// g_skinny_cfg (cgemm_4bit_set_skinny_config, lab A/B): -1 = that rule, 0 = base, 1 = 8 waves same NB, 2 = 8 waves 2 x NB.
+static int g_skinny_cfg = -1;
+
+struct SkGeom {
+  int cfg, waves, nb, splits;
+};
+
+int device_cu_count();   // CUs of the current device (cached; gemv4bit.hip)
+
+static SkGeom skinny_geometry(int m, int n, int k) {
+  const int mt = skinny_tiles(n), kb = k / 128;
+  const int nb = mt == 1 ? skinny_nb<1>() : (mt == 2 ? skinny_nb<2>() : skinny_nb<4>());
+  int cfg = g_skinny_cfg;
+  if (cfg < 0) {
+    cfg = 0;
+    if (mt == 4) {
+      const long long wg = (long long)((m + 127) / 128) * ((kb + 2 * nb - 1) / (2 * nb));
+      const long long cus = device_cu_count(), rounds = (wg + cus - 1) / cus;
+      if (10 * wg >= 7 * rounds * cus) cfg = 2;
+    }
+  }
+  const int nbw = cfg == 2 ? 2 * nb : nb;
+  return SkGeom{cfg, cfg == 0 ? 4 : 8, nbw, (kb + nbw - 1) / nbw};
 }
 
+// workspace for any geometry: the base form has the most splits
 long long skinny_workspace_bytes(int m, int n, int k) {
   if (n < 1 || n > SK_MAX_TOKENS || k < 128 || k % 128) return 0;
-  const int s = skinny_splits(n, k);
+  const int mt = skinny_tiles(n), nb = mt == 1 ? skinny_nb<1>() : (mt == 2 ? skinny_nb<2>() : skinny_nb<4>());
+  const int s = (k / 128 + nb - 1) / nb;
   return s > 1 ? (long long)s * n * m * (long long)sizeof(float) : 0;
 }
 
@@ -289,26 +322,37 @@ bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uin
   if (!skinny_applicable(m, n, k, lda, ldb, blocksize, A, B)) return false;
   const bool nested = st.q8 != nullptr;
   if (nested && (blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1)))) return false;
-  const int s = skinny_splits(n, k);
+  const SkGeom geo = skinny_geometry(m, n, k);
+  const int s = geo.splits;
   if (s > 1 && (ws == nullptr || ((uintptr_t)ws & 15) || (long long)s * n * m * (long long)sizeof(float) > ws_bytes))
     return false;
   st.bs_shift = __builtin_ctz(blocksize);
   st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
-  const dim3 grid((unsigned)(((m + SK_ROWS - 1) / SK_ROWS) * s));
+  const int waves = geo.waves;
+  const dim3 grid((unsigned)(((m + 16 * waves - 1) / (16 * waves)) * s));
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(SK_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, ws, out,
+    hipLaunchKernelGGL(kern, grid, dim3(64 * waves), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, ws, out,
                        ldc, s);
   };
   const int mt = skinny_tiles(n);
-  if (nested) {
-    if (mt == 1) go(k_gemm_4bit_skinny<T, 1, skinny_nb<1>(), true>);
-    else if (mt == 2) go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), true>);
-    else go(k_gemm_4bit_skinny<T, 4, skinny_nb<4>(), true>);
-  } else {
-    if (mt == 1) go(k_gemm_4bit_skinny<T, 1, skinny_nb<1>(), false>);
-    else if (mt == 2) go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), false>);
-    else go(k_gemm_4bit_skinny<T, 4, skinny_nb<4>(), false>);
-  }
+  auto dispatch = [&](auto nested_tag) {
+    constexpr bool NS = decltype(nested_tag)::value;
+    if (geo.cfg == 0) {
+      if (mt == 1) go(k_gemm_4bit_skinny<T, 1, skinny_nb<1>(), NS>);
+      else if (mt == 2) go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), NS>);
+      else go(k_gemm_4bit_skinny<T, 4, skinny_nb<4>(), NS>);
+    } else if (geo.cfg == 1) {
+      if (mt == 1) go(k_gemm_4bit_skinny<T, 1, skinny_nb<1>(), NS, 0, 8>);
+      else if (mt == 2) go(k_gemm_4bit_skinny<T, 2, skinny_nb<2>(), NS, 0, 8>);
+      else go(k_gemm_4bit_skinny<T, 4, skinny_nb<4>(), NS, 0, 8>);
+    } else {
+      if (mt == 1) go(k_gemm_4bit_skinny<T, 1, 2 * skinny_nb<1>(), NS, 0, 8>);
+      else if (mt == 2) go(k_gemm_4bit_skinny<T, 2, 2 * skinny_nb<2>(), NS, 0, 8>);
+      else go(k_gemm_4bit_skinny<T, 4, 2 * skinny_nb<4>(), NS, 0, 8>);
+    }
+  };
+  if (nested) dispatch(std::true_type{});
+  else dispatch(std::false_type{});
   if (s > 1) {
     const long long mn = (long long)m * n;
     hipLaunchKernelGGL((k_skinny_reduce<T>), dim3((unsigned)((mn / 4 + 255) / 256 + 1)), dim3(256), 0, current_stream(), ws, s,
@@ -327,6 +371,10 @@ template bool launch_gemm_4bit_skinny<fp16_t>(int, int, int, const fp16_t*, int,
 using namespace bnb;
 
 extern "C" {
+
+// [lab, not in the header] A/B knob of the few-token split-K kernel's geometry: -1 = the measured rule (default),
+// 0 / 1 / 2 = forced (see g_skinny_cfg)
+void cgemm_4bit_set_skinny_config(int cfg) { bnb::g_skinny_cfg = cfg; }
 
 // [additive] few-token 4-bit GEMM with compressed statistics decoded in-kernel (one launch instead of
 // the absmax decode + GEMM; functional.py:1346-1350 order).  Returns 0 when launched, 1 when the shape,

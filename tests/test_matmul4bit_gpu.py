@@ -631,6 +631,42 @@ def test_fewtoken_whole_k_and_split_k_kernels(dev, dtype, nested, mnk):
         F.GEMM_4BIT_GEMV_TOKENS = saved
 
 
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("mnk", [(40, 1001, 2048), (64, 4096, 11008), (33, 4099, 4096), (12, 300, 1152), (24, 130, 256),
+                                 (64, 129, 128), (48, 1024, 8192)])
+def test_fewtoken_split_k_geometries(dev, nested, mnk):
+    """The split-K few-token kernel in each workgroup geometry (cgemm_4bit_set_skinny_config 0 / 1 / 2: 4 waves, 8
+    waves with the same blocks per split, 8 waves with twice the blocks per split) and the default rule (-1): every
+    form within the oracle tolerance; the forms with the same splits give the same bits (per-row summation order is
+    unchanged).  Covers ragged out_features below and above one 128-row workgroup, one-split K and 1 / 2 / 4 token tiles."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M * 7 + N)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), F._absmax_fp32(st).cpu().numpy(), N, K,
+                                    64, st.code.cpu().numpy(), "bf16")
+    saved = F.GEMM_4BIT_GEMV_TOKENS
+    F.GEMM_4BIT_GEMV_TOKENS = 1
+    outs = {}
+    try:
+        F.lib.cgemm_4bit_set_fewtoken_kernel(1)
+        for cfg in (0, 1, 2, -1):
+            F.lib.cgemm_4bit_set_skinny_config(cfg)
+            Y = F.gemm_4bit(X, q, st)
+            torch.cuda.synchronize()
+            assert F.lib.cget_last_error() == 0
+            frac, err = _close(Y.float().cpu().numpy(), exp, 2e-2, 2e-2)
+            assert frac == 0.0, (cfg, err)
+            outs[cfg] = Y
+        assert torch.equal(outs[0], outs[1])
+    finally:
+        F.lib.cgemm_4bit_set_skinny_config(-1)
+        F.lib.cgemm_4bit_set_fewtoken_kernel(0)
+        F.GEMM_4BIT_GEMV_TOKENS = saved
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("mnk", [(2048, 1024, 2048), (300, 520, 640), (4096, 11008, 4096), (1, 64, 64)])
 def test_library_gemm_solution_search(dev, dtype, mnk):

@@ -359,7 +359,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(code, hc.data(), 64, hipMemcpyHostToDevice));
   }
   const int MT = M <= 16 ? 1 : 2;
-  const int s = skinny_splits(M, K);
+  const int s = skinny_geometry(N, M, K).splits;   // base form at these token counts
   const int grid = ((N + SK_ROWS - 1) / SK_ROWS) * s;
   // the library kernel stamps every launch (SK_STAMP): its buffer is set before the first launch
   unsigned long long* st; CK(hipMalloc(&st, (size_t)grid * 4 * 3 * 8));

@@ -32,7 +32,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(X, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
     float hc[16]; for (int i = 0; i < 16; ++i) hc[i] = (i - 7.5f) / 8; CK(hipMemcpy(code, hc, 64, hipMemcpyHostToDevice));
   }
-  const int s = skinny_splits(M, K);
+  const int s = skinny_geometry(N, M, K).splits;   // base form at these token counts
   const int grid = ((N + SK_ROWS - 1) / SK_ROWS) * s;
   printf("N=%d K=%d M=%d: %d splits, %d workgroups, weights %.1f MB\n", N, K, M, s, grid, N * (double)K / 2e6);
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
