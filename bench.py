@@ -320,12 +320,7 @@ def bench_nf4_fused_kernel(dev, m=M, n=N, k=K, iters=20):
     del W
     Y = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
     am = F._absmax_fp32(st)
-    saved = F.GEMM_4BIT_DEQUANT_MIN_ROWS
-    F.GEMM_4BIT_DEQUANT_MIN_ROWS = 1 << 30
-    try:
-        t = _time_loop(lambda: F.gemm_4bit(X, q, st, out=Y, absmax=am), iters)
-    finally:
-        F.GEMM_4BIT_DEQUANT_MIN_ROWS = saved
+    t = _time_loop(lambda: F.gemm_4bit(X, q, st, out=Y, absmax=am, _route="fused"), iters)
     flops = 2.0 * m * n * k
     return {"shape": [m, n, k], "kernel": "k_gemm_4bit_256<bf16>", "us": t * 1e6, "tflops": flops / t / 1e12,
             "frac_of_bf16_peak": flops / t / 1e12 / PEAK_BF16_TFLOPS}

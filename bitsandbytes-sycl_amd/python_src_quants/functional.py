@@ -744,7 +744,7 @@ GEMM_4BIT_GEMV_TOKENS = 4
 # searched rocBLAS solution 1.45; at 1536 rows the fused kernel's 258 tiles take two passes over 256 CUs and the pair
 # is 1.5-1.7x faster (profiles/lab/r02_lib_route.txt, r02_rocblas_solutions.txt, r02_mid_rows_route.txt).  So the
 # first call of a shape (per device, dtype and statistics format) times three routes on its own operands (one warm
-# call, best of two timed): "library" (dequantise + torch.matmul, torch's hipBLASLt heuristic), "library_tn"
+# call each, then the best of three interleaved rounds): "library" (dequantise + torch.matmul, torch's hipBLASLt heuristic), "library_tn"
 # (dequantise + cgemm_tn_*, rocBLAS with the per-shape solution search of gemm_lib.hip) and "fused" (the hand-written
 # kernel), and leaves the static rule's route only for one faster by more than GEMM_4BIT_ROUTE_MARGIN; during
 # HIP-graph capture nothing is timed and the static rule stands.  The choice is cached
@@ -787,19 +787,18 @@ def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax:
         return route
     if torch.cuda.is_current_stream_capturing():
         return default
-    times = {}
-    for name in ("library", "library_tn", "fused"):
+    names = ("library", "library_tn", "fused")
+    for name in names:          # untimed: code-object loads, the rocBLAS solution search, workspaces, clock ramp
         gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
-        best = None
-        for _ in range(2):
+    times = {name: float("inf") for name in names}
+    for _ in range(3):          # interleaved rounds, best per route (no route is timed only on a colder clock)
+        for name in names:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
             e.record()
             e.synchronize()
-            t = s.elapsed_time(e)
-            best = t if best is None else min(best, t)
-        times[name] = best
+            times[name] = min(times[name], s.elapsed_time(e))
     fastest = min(times, key=times.get)
     route = fastest if times[fastest] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times[default] else default
     _ROUTES[key] = route

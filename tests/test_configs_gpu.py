@@ -57,6 +57,7 @@ def test_metric_shape(dev, route, monkeypatch):
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=torch.Generator(device=dev).manual_seed(1))
     if route == "fused":
         monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1 << 30)
+        monkeypatch.setattr(F, "GEMM_4BIT_ROUTE_TUNING", False)
     Y = F.gemm_4bit(X, q, st)
     _check_rows(Y, X, q, F._absmax_fp32(st), N, K, st.code, _sample_rows(M, dev))
 

@@ -21,6 +21,14 @@ def _F():
     return F
 
 
+@pytest.fixture(autouse=True)
+def _static_route(monkeypatch):
+    """These are kernel tests: pin the static route rule, so a shape above the few-token range reaches the kernel under
+    test instead of whichever route the measurement (functional.GEMM_4BIT_ROUTE_TUNING) found faster on this box.
+    The measured route itself is tested in test_configs_gpu.py."""
+    monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
+
+
 def _lib_matmul(F, X, Wd):
     """X @ Wd^T through the library GEMM the product's large-prefill route uses (cgemm_tn_*, gemm_lib.hip) with the
     plan cached for this shape: the reference's F.linear on the dequantised weight."""
@@ -172,6 +180,7 @@ def test_gemm_4bit_tile_kernels_agree_large(dev, monkeypatch):
     (the fused kernel forced: at this size gemm_4bit would take the dequantise + library GEMM path)."""
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1 << 30)
+    monkeypatch.setattr(F, "GEMM_4BIT_ROUTE_TUNING", False)
     M, N, K = 2048, 2048, 11008
     torch.manual_seed(11)
     W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
