@@ -355,6 +355,56 @@ def bench_llama2_7b_prefill(dev, batch=32, seq=2048, iters=3):
     return res
 
 
+def bench_llama2_70b_shard(dev, ranks=8, prefill_tokens=4096, layer_copies=8, iters=3):
+    """Config 5 on one GPU: the rank-local work of one Llama-2-70B decoder layer column-sharded 8 ways (the seven
+    Linear4bit NF4 projections, nested statistics; hidden 8192, GQA k/v 1024, MLP 28672; each rank holds N/8 output
+    columns: q/o 1024 x 8192, k/v 128 x 8192, gate/up 3584 x 8192, down 1024 x 28672), at a 4096-token prefill and
+    at 1-token decode, through functional.gemm_4bit / gemv_4bit as Linear4bit calls them.  The bf16 all-gather of
+    the shards (parallel.py) is not in these numbers: the multi-GPU bench times it.  Decode: `layer_copies` distinct
+    layers (> the 256 MB MALL) replayed from one HIP graph, GB/s over the packed weights + statistics read."""
+    hid, kv, inter = 8192, 1024, 28672
+    shapes = [(hid // ranks, hid), (kv // ranks, hid), (kv // ranks, hid), (hid // ranks, hid),
+              (inter // ranks, hid), (inter // ranks, hid), (hid // ranks, inter)]
+    g = torch.Generator(device=dev).manual_seed(8)
+    layers = []
+    for _ in range(layer_copies):
+        ws = []
+        for n_out, k_in in shapes:
+            W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+            ws.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True))
+            del W
+        layers.append(ws)
+    res = {"rank_shapes": [[n, k] for n, k in shapes], "ranks": ranks}
+    # prefill: one layer, 4096 tokens
+    X = torch.randn(prefill_tokens, hid, device=dev, dtype=torch.bfloat16, generator=g)
+    Xi = torch.randn(prefill_tokens, inter, device=dev, dtype=torch.bfloat16, generator=g)
+    outs = {n: torch.empty(prefill_tokens, n, device=dev, dtype=torch.bfloat16) for n, _ in shapes}
+
+    def layer():
+        for (n_out, k_in), (q, st) in zip(shapes, layers[0]):
+            F.gemm_4bit(X if k_in == hid else Xi, q, st, out=outs[n_out])
+    t = _time_loop(layer, iters)
+    flops = sum(2.0 * prefill_tokens * n * k for n, k in shapes)
+    res["prefill"] = {"tokens": prefill_tokens, "layer_ms": t * 1e3, "tflops": flops / t / 1e12,
+                      "model_80_layers_ms": 80 * t * 1e3}
+    del X, Xi, outs
+    # decode: one token through every projection of `layer_copies` layers
+    x, xi = (torch.randn(1, k, device=dev, dtype=torch.bfloat16, generator=g) for k in (hid, inter))
+    dec_out = {n: torch.empty(1, n, device=dev, dtype=torch.bfloat16) for n, _ in shapes}
+    calls = [(lambda q=q, st=st, n=n, k=k: F.gemv_4bit(x if k == hid else xi, q.t(), out=dec_out[n], state=st))
+             for ws in layers for (n, k), (q, st) in zip(shapes, ws)]
+    t_call = _time_graph(calls, 10)
+    t_layer = t_call * len(shapes)
+    wbytes = sum(n * k // 2 + n * k // BS + n * k // BS // 256 * 4 + 1024 for n, k in shapes)
+    res["decode"] = {"layer_us": t_layer * 1e6, "weight_bytes_per_layer": wbytes, "gbs": wbytes / t_layer / 1e9,
+                     "frac_of_hbm": wbytes / t_layer / 1e9 / PEAK_HBM_GBS, "model_80_layers_ms": 80 * t_layer * 1e3}
+    res["note"] = ("rank-local compute only (no all-gather); decode over 8 distinct layers (~430 MB) from one HIP "
+                   "graph; prefill path per shape from the measured route")
+    del layers, calls
+    torch.cuda.empty_cache()
+    return res
+
+
 def host_cpu_info():
     """The GPU box's host CPU as the bench sees it: model name (/proc/cpuinfo), logical CPUs of the machine and
     the CPUs this process may run on (the box gives a job a share of a larger machine)."""
@@ -611,6 +661,7 @@ def main():
         extras["optimizer_adam8bit_blockwise"] = bench_optimizer_8bit(dev)
         extras["nf4_fused_kernel_metric_shape"] = bench_nf4_fused_kernel(dev)
         extras["llama2_7b_prefill_config4"] = bench_llama2_7b_prefill(dev)
+        extras["llama2_70b_rank_shard_config5"] = bench_llama2_70b_shard(dev)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.no_extras:
         try:

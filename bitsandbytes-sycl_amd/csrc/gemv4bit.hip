@@ -395,6 +395,103 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
   }
 }
 
+// Wide GEMV (narrow or long-K weights: the 70B shards, e.g. 1024 x 28672 and 128 x 8192): one workgroup per weight
+// row, its NW waves split K (lane t of the workgroup takes chunks t + 64 NW u, u < U), summed across waves in LDS in
+// wave order.  The balanced kernel gives a workgroup whole rows, so a few hundred rows leave most of the chip idle, and
+// K > GV_MAX_K does not fit its LDS activation copy; here the activations come from L2 (each workgroup reads all
+// of x) and only the pair table sits in LDS (the 128-B-stride copies of k_gemv_4bit_dot, conflict-free).  Same
+// per-chunk arithmetic as the other table kernels; the chunk-to-lane grouping, and so the fp32 summation order, differs.
+constexpr int GW_MAX_WAVES = 16;
+
+template <typename T, int U, bool NESTED>
+__global__ void __launch_bounds__(GW_MAX_WAVES * 64)
+k_gemv_4bit_wide(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
+                 const float* __restrict__ datatype, T* __restrict__ out, int ldb) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
+  uint8_t* table = gsm;                                           // GV_TABLE_BYTES
+  float* code2s = reinterpret_cast<float*>(gsm + GV_TABLE_BYTES); // 256 (nested)
+  float* red = code2s + 256;                                      // one partial per wave
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int NT = blockDim.x, NW = NT >> 6;
+  const int row = blockIdx.x;
+  const int nch = K >> 5;
+  const long long two_ldb = 2LL * ldb;
+  auto chunk_of = [&](int u) { return min(tid + NT * u, nch - 1); };
+  // (1) statistics, activations (L2), then the weights (non-temporal)
+  float am[U];
+  uint32_t q8[U];
+  float a2[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long blk = (two_ldb * row + 32LL * chunk_of(u)) >> st.bs_shift;
+    if constexpr (NESTED) {
+      q8[u] = st.q8[blk];
+      a2[u] = st.absmax2[blk >> st.bs2_shift];
+    } else {
+      am[u] = st.absmax[blk];
+    }
+  }
+  float offset = 0.0f;
+  if constexpr (NESTED) offset = *st.offset;
+  uint4 xv[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xv[u][q] = reinterpret_cast<const uint4*>(A + 32 * chunk_of(u))[q];
+  uintptr_t bp = (uintptr_t)B;
+  asm volatile("" : "+s"(bp)::"memory");
+  uint4 b[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const u32x4_t v = __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row * ldb + 16LL * chunk_of(u)));
+    b[u] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+  // (2) table: 16-B store i holds entry i >> 3 for copies 4 (i & 7) .. 4 (i & 7) + 3 (entry e of copy j at 128 e + 4 j)
+  for (int i = tid; i < GV_TABLE_BYTES / 16; i += NT) {
+    const int e = i >> 3;
+    const uint32_t v = Dot2<T>::pair(datatype[e >> 4], datatype[e & 15]);
+    *reinterpret_cast<uint4*>(table + 16 * i) = make_uint4(v, v, v, v);
+  }
+  if constexpr (NESTED)
+    for (int t = tid; t < 256; t += NT) code2s[t] = st.code2[t];
+  __syncthreads();
+  if constexpr (NESTED) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) am[u] = __fadd_rn(__fmul_rn(code2s[q8[u]], a2[u]), offset);
+  }
+  // (3) dot: per chunk s0 / s1 chains of v_dot2 over 16 packed bytes, scaled by the chunk's absmax
+  const uint32_t lane4 = (lane & 31) * 4;
+  float acc = 0.0f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t x[16] = {xv[u][0].x, xv[u][0].y, xv[u][0].z, xv[u][0].w, xv[u][1].x, xv[u][1].y, xv[u][1].z,
+                            xv[u][1].w, xv[u][2].x, xv[u][2].y, xv[u][2].z, xv[u][2].w, xv[u][3].x, xv[u][3].y,
+                            xv[u][3].z, xv[u][3].w};
+    const uint32_t w[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
+    uint32_t l[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      l[i] = *reinterpret_cast<const uint32_t*>(table + ((((w[i >> 2] >> (8 * (i & 3))) & 0xFF) << 7) | lane4));
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      s0 = Dot2<T>::dot(x[i], l[i], s0);
+      s1 = Dot2<T>::dot(x[i + 1], l[i + 1], s1);
+    }
+    const float part = (s0 + s1) * am[u];
+    acc += (tid + NT * u < nch) ? part : 0.0f;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) red[wave] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    float s = red[0];
+    for (int w2 = 1; w2 < NW; ++w2) s += red[w2];
+    out[row] = Io<T>::from_f32(s);
+  }
+}
+
 // General path (any K, ldb, alignment): one wave per row, one element per lane step.
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -414,7 +511,10 @@ k_gemv_4bit_generic(int M, int K, const T* __restrict__ A, const uint8_t* __rest
   if (lane == 0) out[row] = Io<T>::from_f32(acc);
 }
 
-int g_gemv_kernel = 0;   // 0 = auto (k_gemv_4bit_bal where it fits), 1 = k_gemv_4bit_dot only (A/B, tests)
+// 0 = auto (k_gemv_4bit_wide on narrow / long-K weights, k_gemv_4bit_bal where it fits, else k_gemv_4bit_dot),
+// 1 = k_gemv_4bit_dot only, 2 = k_gemv_4bit_wide wherever it applies, 3 = auto without the wide kernel (A/B, tests);
+// 20 + U: the wide kernel with U chunks per lane (lab)
+int g_gemv_kernel = 0;
 
 int device_cu_count() {
   static int cus = 0;
@@ -476,6 +576,44 @@ static bool launch_gemv_bal(int m, int k, const T* A, const uint8_t* B, const Ge
 }
 
 
+// k_gemv_4bit_wide: NW waves per row such that each lane holds U chunks; false when K needs more than 16 waves x 4
+// chunks (K > 131072)
+template <typename T, bool NESTED>
+static bool launch_gemv_wide(int m, int k, const T* A, const uint8_t* B, const GemvStats& st, const float* datatype,
+                             T* out, int ldb) {
+  const int nch = k >> 5;
+  // measured (tools/gemv_shape_probe.py, profiles/lab/r02_gemv_wide.txt): 4 chunks per lane on long K (1024 x 28672:
+  // 13.3 / 11.6 / 12.0 / 10.3 us at U = 1..4), 1 on short K (128 x 8192: 3.8 / 4.5 / 4.9 / 6.5 us)
+  int U = g_gemv_kernel >= 21 && g_gemv_kernel <= 24 ? g_gemv_kernel - 20 : (k > GV_MAX_K ? 4 : 1);
+  int nw = (nch + 64 * U - 1) / (64 * U);
+  if (nw > GW_MAX_WAVES) {
+    nw = GW_MAX_WAVES;
+    U = (nch + 64 * nw - 1) / (64 * nw);
+  }
+  if (U > 4) return false;
+  nw = (nch + 64 * U - 1) / (64 * U);
+  const size_t lds = GV_TABLE_BYTES + 256 * sizeof(float) + GW_MAX_WAVES * sizeof(float);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)m), dim3(64 * nw), lds, current_stream(), m, k, A, B, st, datatype, out, ldb);
+    return true;
+  };
+  switch (U) {
+    case 1: return go(k_gemv_4bit_wide<T, 1, NESTED>);
+    case 2: return go(k_gemv_4bit_wide<T, 2, NESTED>);
+    case 3: return go(k_gemv_4bit_wide<T, 3, NESTED>);
+    default: return go(k_gemv_4bit_wide<T, 4, NESTED>);
+  }
+}
+
+// the wide kernel by default: K beyond the balanced kernel's LDS (1024 x 28672, the 70B down-projection shard: 26.9
+// -> 10.3 us), or fewer rows than CUs (128 x 8192, the 70B k/v shard: 5.2 -> 3.8 us).  From a few hundred rows
+// its per-row table fill loses to the balanced kernel (1024 x 8192 4.0 vs 5.1 us, 11008 x 4096 8.1 vs 41 us).
+static bool gemv_wide_preferred(int m, int k) {
+  if (g_gemv_kernel == 2 || (g_gemv_kernel >= 21 && g_gemv_kernel <= 24)) return true;
+  if (g_gemv_kernel != 0) return false;
+  return k > GV_MAX_K || m < device_cu_count();
+}
+
 // Launch the table/dot kernel when the shape fits it; false -> caller uses another kernel.
 template <typename T>
 bool launch_gemv_dot(int m, int k, const T* A, const uint8_t* B, GemvStats st, const float* datatype, T* out, int ldb,
@@ -483,10 +621,15 @@ bool launch_gemv_dot(int m, int k, const T* A, const uint8_t* B, GemvStats st, c
   const bool nested = st.q8 != nullptr;
   if (k % 32 || ldb % 16 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || blocksize < 32) return false;
   if ((blocksize & (blocksize - 1)) || (nested && (blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1))))) return false;
-  const size_t lds = GV_TABLE_BYTES + 2 * (size_t)k + (nested ? 1024 : 0);
-  if (k > GV_MAX_K || lds > 65536) return false;
   st.bs_shift = __builtin_ctz(blocksize);
   st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
+  if (gemv_wide_preferred(m, k)) {
+    const bool ok = nested ? launch_gemv_wide<T, true>(m, k, A, B, st, datatype, out, ldb)
+                           : launch_gemv_wide<T, false>(m, k, A, B, st, datatype, out, ldb);
+    if (ok) return true;
+  }
+  const size_t lds = GV_TABLE_BYTES + 2 * (size_t)k + (nested ? 1024 : 0);
+  if (k > GV_MAX_K || lds > 65536) return false;
   if (g_gemv_kernel != 1) {
     const bool ok = nested ? launch_gemv_bal<T, true>(m, k, A, B, st, datatype, out, ldb)
                            : launch_gemv_bal<T, false>(m, k, A, B, st, datatype, out, ldb);

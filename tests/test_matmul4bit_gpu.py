@@ -492,13 +492,55 @@ def test_gemv_balanced_kernel_matches_dot_kernel(dev, dtype, nested, shape, quan
     W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
     q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
     x = torch.randn(1, K, device=dev, dtype=dtype)
-    y_auto = F.gemv_4bit(x, q.t(), state=st)
-    F.lib.cgemv_4bit_set_kernel(1)
     try:
+        F.lib.cgemv_4bit_set_kernel(3)          # the automatic choice without the wide kernel
+        y_auto = F.gemv_4bit(x, q.t(), state=st)
+        F.lib.cgemv_4bit_set_kernel(1)
         y_dot = F.gemv_4bit(x, q.t(), state=st)
     finally:
         F.lib.cgemv_4bit_set_kernel(0)
     assert torch.equal(y_auto.view(torch.int16), y_dot.view(torch.int16))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(1024, 28672), (128, 8192), (37, 40960), (7, 64), (200, 2080), (3, 131072),
+                                   (1000, 4096)])
+@pytest.mark.parametrize("quant", [("nf4", 64), ("fp4", 128)])
+def test_gemv_wide_kernel(dev, dtype, shape, quant):
+    """k_gemv_4bit_wide (one workgroup per row, K split over its waves, summed in wave order): the default for K
+    beyond the balanced kernel's LDS and for fewer rows than CUs, forced here on every shape (1000 x 4096 would take
+    the balanced kernel).  Within the oracle tolerance for plain and compressed statistics, the in-kernel decode
+    bit-identical to the decoded-absmax call, and the default route equal to the forced one where it is taken."""
+    F = _F()
+    N, K = shape
+    qt, bs = quant
+    torch.manual_seed(N + K + bs)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    x = torch.randn(1, K, device=dev, dtype=dtype)
+    name = {torch.bfloat16: "bf16", torch.float16: "fp16"}[dtype]
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    for nested in (False, True):
+        q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
+        absmax = F._absmax_fp32(st)
+        exp = ref.gemv_4bit(x.float().cpu().numpy()[0], q.cpu().numpy(), absmax.cpu().numpy(), N, K, bs,
+                            st.code.cpu().numpy())
+        y_default = F.gemv_4bit(x, q.t(), state=st)
+        F.lib.cgemv_4bit_set_kernel(2)
+        try:
+            y = F.gemv_4bit(x, q.t(), state=st)
+            two_step = torch.empty_like(y)
+            getattr(F.lib, f"cgemm_4bit_inference_naive_{name}")(
+                ct.c_int32(N), ct.c_int32(1), ct.c_int32(K), F.get_ptr(x), F.get_ptr(q), F.get_ptr(absmax),
+                F.get_ptr(st.code), F.get_ptr(two_step), ct.c_int32(N), ct.c_int32(K // 2), ct.c_int32(N), ct.c_int32(bs))
+            torch.cuda.synchronize()
+        finally:
+            F.lib.cgemv_4bit_set_kernel(0)
+        assert F.lib.cget_last_error() == 0
+        frac, err = _close(y.float().cpu().numpy()[0], exp, tol, tol)
+        assert frac == 0.0, (nested, err)
+        assert torch.equal(y.view(torch.int16), two_step.view(torch.int16))
+        if K > 16384 or N < 256:
+            assert torch.equal(y_default.view(torch.int16), y.view(torch.int16))
 
 
 @pytest.mark.parametrize("nested", [False, True])
@@ -549,9 +591,13 @@ def test_gemm_4bit_multirow_gemv_matches_gemv(dev, dtype, nested, rows, shape):
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
     Y = F.gemm_4bit(X, q, st)
     assert Y.shape == (rows, N)
-    for t in range(rows):
-        y = F.gemv_4bit(X[t:t + 1], q.t(), state=st)
-        assert torch.equal(Y[t], y.reshape(-1)), f"row {t} differs from gemv_4bit"
+    F.lib.cgemv_4bit_set_kernel(3)              # the balanced / dot GEMV family (not the wide kernel of narrow weights)
+    try:
+        for t in range(rows):
+            y = F.gemv_4bit(X[t:t + 1], q.t(), state=st)
+            assert torch.equal(Y[t], y.reshape(-1)), f"row {t} differs from gemv_4bit"
+    finally:
+        F.lib.cgemv_4bit_set_kernel(0)
 
 
 @pytest.mark.parametrize("nested", [False, True])
