@@ -162,9 +162,11 @@ int g_tile_override = 0;
 // Split-K factor for the 256-tile kernel: enough workgroups to cover the 256 CUs when the output has
 // fewer than ~200 256x256 tiles (narrow column shards, e.g. N/8 = 512 features at M = 4096, or few
 // tokens: 16 x 4096 x 11008 ran 176 us on the 32-workgroup 128-tile grid), with at least 8 k-tiles
-// per split.  Needs a caller-supplied fp32 workspace of ksplit * m * n floats.
+// per split.  Below 256 weight rows (the 70B k/v shard 128 x 8192 at 4096 tokens: 16 half-empty tiles) the split
+// form still beats the 128-tile kernel's 32 whole-K workgroups (151 us there; profiles/lab/r02_narrow_weight.txt).
+// Needs a caller-supplied fp32 workspace of ksplit * m * n floats.
 static int splitk_factor(int m, int n, int k) {
-  if (m < 256) return 1;
+  if (m < 64) return 1;
   const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
   if (tiles >= 200) return 1;
   int ks = (int)((256 + tiles / 2) / tiles);
@@ -205,7 +207,7 @@ void gemm_4bit(int m, int n, int k, const T* A, const uint8_t* B, const float* a
   // 256 tokens: 8 workgroups of 128x128 took 174 us where 2 x 16-way split 256x256 tiles take ~25)
   const long long tiles128 = (long long)((m + G_BN - 1) / G_BN) * ((n + G_BM - 1) / G_BM);
   const bool use256 = pow2_bs && (g_tile_override == 256 ||
-                                  (g_tile_override != 128 && m >= 256 &&
+                                  (g_tile_override != 128 && (m >= 256 || ks > 1) &&
                                    (tiles256 * ks >= 128 || 2 * tiles256 * ks >= tiles128)));
   if (use256) {
     launch_gemm_4bit_256<T>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, ws, ks);

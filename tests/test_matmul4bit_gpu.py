@@ -154,6 +154,34 @@ def test_gemm_4bit_vs_oracle(dev, dtype, qt, mnk):
     assert (Y.float() - Yref).abs().mean().item() < 0.115
 
 
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("mnk", [(1024, 128, 2048), (2000, 100, 4096), (4096, 200, 1024), (700, 64, 8192)])
+def test_gemm_4bit_narrow_weight_split_k(dev, nested, mnk):
+    """Fewer than 256 weight rows at prefill sizes (the 70B k/v shard, 128 x 8192): the 256-tile kernel in its
+    split-K form (half-empty tiles, clamped loads, guarded stores) instead of 32 whole-K 128-tile workgroups --
+    within the oracle tolerance on every output, and equal to the 128-tile kernel up to fp32 summation order."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M + N + K)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    Y = F.gemm_4bit(X, q, st)
+    torch.cuda.synchronize()
+    assert F.lib.cget_last_error() == 0
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), F._absmax_fp32(st).cpu().numpy(), N, K,
+                                    64, st.code.cpu().numpy(), "bf16")
+    frac, err = _close(Y.float().cpu().numpy(), exp, 2e-2, 2e-2)
+    assert frac == 0.0, err
+    F.lib.cgemm_4bit_set_tile(128)
+    try:
+        Y128 = F.gemm_4bit(X, q, st)
+    finally:
+        F.lib.cgemm_4bit_set_tile(0)
+    rms = Y128.float().pow(2).mean().sqrt().item()
+    assert (Y.float() - Y128.float()).abs().max().item() < 1e-2 * rms + 1e-2 * Y128.float().abs().max().item()
+
+
 @pytest.mark.parametrize("tile", [128, 256])
 @pytest.mark.parametrize("mnk", [(256, 256, 128), (300, 520, 640), (1000, 384, 256)])
 def test_gemm_4bit_each_tile_kernel(dev, tile, mnk):
