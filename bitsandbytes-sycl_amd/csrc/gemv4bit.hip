@@ -261,11 +261,16 @@ k_gemv_4bit_dot(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
 //     ds_read_b128 of chunks lane + 64u is conflict-free (4-way on the plain layout);
 //   * every wave issues its statistics and activation loads, then a barrier, then its weights: the CU's
 //     request queue holds all of the former ahead of any weight request.
-// LDS: 64 KiB table + 2K activations (+ 1 KiB nested code map): two workgroups per CU up to K = 7680 (7168
-// nested), one workgroup of up to 16 waves per CU above that (K <= 16384).
+// LDS: 64 KiB table + 2K activations (the nested code map sits in the table's spare halves): two workgroups per CU
+// up to K = 8192 (exactly half the CU's LDS each), one workgroup of up to 16 waves per CU above that (K <= 16384).
 constexpr int GB_TABLE_BYTES = 65536;
 constexpr int GB_MAX_WAVES = 16;
-constexpr size_t GB_TWO_PER_CU_LDS = 80 * 1024 - 1024;   // two workgroups per CU with room to spare
+// two workgroups per CU up to 79 KiB (K <= 7680), and at exactly half the CU's 160 KiB (K = 8192) from 2048 rows:
+// 3584 / 4096 / 8192 x 8192 6.20 / 6.79 / 10.77 -> 6.00 / 6.34 / 10.43 us, but 1024 x 8192 4.00 -> 5.04 us, where
+// two table fills per CU outweigh the gain (profiles/lab/r02_gemv_wide.txt).  Lab knob: cgemv_4bit_set_two_per_cu_lds.
+static size_t g_gb_two_per_cu_lds = 79 * 1024;
+constexpr size_t GB_HALF_CU_LDS = 80 * 1024;
+constexpr int GB_HALF_CU_MIN_ROWS = 2048;
 
 template <typename T, int R, int U, bool NESTED>
 __global__ void __launch_bounds__(GB_MAX_WAVES * 64)
@@ -274,7 +279,11 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
   extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
   uint8_t* table = gsm;                               // GB_TABLE_BYTES
   uint8_t* xs = gsm + GB_TABLE_BYTES;                 // K * 2 bytes, swizzled
-  float* code2s = reinterpret_cast<float*>(xs + 2 * K);
+  // nested code map entry t in the unused upper half of table row t >> 5 (the copies fill bytes 0..127 of each
+  // 256-B entry row), so the map costs no LDS of its own
+  auto code2s_at = [&](uint32_t t) -> float& {
+    return *reinterpret_cast<float*>(table + 256 * (t >> 5) + 128 + 4 * (t & 31));
+  };
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NW = blockDim.x >> 6;
@@ -340,8 +349,8 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * t + 16 * ((k + t) & 7)) = make_uint4(v, v, v, v);
   }
   if constexpr (NESTED) {
-    if (threadIdx.x < 256) code2s[threadIdx.x] = c2;
-    for (int t = threadIdx.x + NW * 64; t < 256; t += NW * 64) code2s[t] = st.code2[t];   // < 4 waves
+    if (threadIdx.x < 256) code2s_at(threadIdx.x) = c2;
+    for (int t = threadIdx.x + NW * 64; t < 256; t += NW * 64) code2s_at(t) = st.code2[t];   // < 4 waves
   }
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * U) : "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -350,7 +359,7 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < R; ++j) am[u][j] = __fadd_rn(__fmul_rn(code2s[q8[u][j]], a2[u][j]), offset);
+      for (int j = 0; j < R; ++j) am[u][j] = __fadd_rn(__fmul_rn(code2s_at(q8[u][j]), a2[u][j]), offset);
   }
   float acc[R];
 #pragma unroll
@@ -534,9 +543,9 @@ int device_cu_count() {
 template <typename T, bool NESTED>
 static bool launch_gemv_bal(int m, int k, const T* A, const uint8_t* B, const GemvStats& st, const float* datatype,
                             T* out, int ldb) {
-  const size_t lds = GB_TABLE_BYTES + 2 * (size_t)k + (NESTED ? 1024 : 0);
+  const size_t lds = GB_TABLE_BYTES + 2 * (size_t)k;     // (+ the nested code map inside the table's spare halves)
   if (k > GV_MAX_K) return false;
-  const bool two = lds <= GB_TWO_PER_CU_LDS;
+  const bool two = lds <= g_gb_two_per_cu_lds || (lds <= GB_HALF_CU_LDS && m >= GB_HALF_CU_MIN_ROWS);
   const int G = min((two ? 2 : 1) * device_cu_count(), m);
   const int rows = (m + G - 1) / G;
   int U = ((k >> 5) + 63) / 64;
@@ -692,6 +701,8 @@ extern "C" {
 
 // [additive, testing] 0 = auto (k_gemv_4bit_bal where it fits), 1 = the 4-waves-x-R-rows kernel only
 void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
+// [lab, not in the header] LDS bytes up to which the balanced GEMV runs two workgroups per CU (default 80 KiB)
+void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size_t)bytes; }
 
 void cgemm_4bit_inference_naive_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax, float* datatype,
                                      fp16_t* out, int lda, int ldb, int ldc, int blocksize) {

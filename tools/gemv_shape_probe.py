@@ -1,7 +1,7 @@
 """Per-shape decode GEMV time (gemv_4bit, nested NF4 bs 64, bf16), `copies` distinct weights replayed from one HIP
 graph, GB/s over packed weights + statistics; per kernel choice (cgemv_4bit_set_kernel: 3 = balanced / dot, 21..24 = the
 wide kernel with 1..4 chunks per lane), max |difference| to the first choice relative to its rms.
-Usage: [GEMV_KNOBS=3,21,22,23,24] python tools/gemv_shape_probe.py [NxK ...]"""
+Usage: [GEMV_KNOBS=3,21,22,23,24] [GEMV_TWO_LDS=bytes] python tools/gemv_shape_probe.py [NxK ...]"""
 import os
 import sys
 
@@ -42,6 +42,8 @@ def graph_us(calls, iters=20):
 def main():
     dev = torch.device("cuda", 0)
     gen = torch.Generator(device=dev).manual_seed(1)
+    if os.environ.get("GEMV_TWO_LDS"):          # lab: LDS bytes up to which the balanced kernel runs 2 per CU
+        F.lib.cgemv_4bit_set_two_per_cu_lds(int(os.environ["GEMV_TWO_LDS"]))
     for n, k in SHAPES:
         copies = max(2, min(64, int(400e6 // (n * k // 2))))
         ws = []
