@@ -180,8 +180,10 @@ bool launch_gemm_4bit_wk(int m, int n, int k, const T* A, int lda, const uint8_t
   // tiles per CU) at any count.  This kernel runs at <= WK_MAX_TOKENS tokens on narrower weights (8 waves per row
   // tile), e.g. 4096 x 11008 at 5 tokens 13.4 vs 16.0 us, 4096 x 4096 8.5 vs 9.3 us; g_fewtoken_kernel = 2 forces
   // it for every 1..32-token shape (tests, A/B).
+  // Not on long K or on very narrow weights either (1024 x 28672 at 2..4 rows 26-29 vs 15.7 us split-K; 128 x 8192
+  // 9.6 vs 8.8 us: profiles/lab/r02_gemv_wide.txt): every workgroup re-reads the token rows of all of K from L2.
   const bool forced = g_fewtoken_kernel == 2;
-  if (!forced && (n > WK_MAX_TOKENS || tiles >= 2 * device_cu_count())) return false;
+  if (!forced && (n > WK_MAX_TOKENS || tiles >= 2 * device_cu_count() || tiles < 64 || k > 16384)) return false;
   const bool wide = tiles >= 2 * device_cu_count();
   const dim3 grid((unsigned)tiles);
   auto go = [&](auto kern, int waves) {

@@ -175,6 +175,9 @@ template <typename T, bool NESTED>
 static bool launch_gemv_tok(int m, int ntok, int k, const T* A, int lda, const uint8_t* B, int ldb, GemvStats st,
                             const float* datatype, T* out, int ldc) {
   if (ntok < 2 || ntok > GT_MAX_TOKENS || k > GV_MAX_K) return false;
+  // fewer weight rows than CUs leave most of the chip idle here (whole rows per workgroup): the split-K few-token
+  // kernel is faster there (128 x 8192 at 4 rows 12.8 -> 9.0 us; profiles/lab/r02_gemv_wide.txt)
+  if (m < device_cu_count()) return false;
   const int tok = ntok <= 2 ? 2 : 4;
   const size_t lds = GT_TABLE_BYTES + (size_t)tok * 2 * k + (NESTED ? 1024 : 0);
   if (lds > 160 * 1024) return false;
