@@ -8,6 +8,7 @@ there is no CPU/torch fallback for them.
 from __future__ import annotations
 
 import ctypes as ct
+import functools
 import os
 import threading
 import weakref
@@ -406,7 +407,8 @@ def dequantize_blockwise(A: Tensor, quant_state: Optional[QuantState] = None, ab
         code = quant_state.code.cpu()
         absmax = absmax.float().contiguous()
         o32 = out if (out.dtype == torch.float32 and out.is_contiguous()) else torch.empty(A.shape, dtype=torch.float32)
-        lib.cdequantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(A.contiguous()), get_ptr(absmax), get_ptr(o32),
+        Ac = A.contiguous()   # bound to a name: the C call must not see a freed temporary
+        lib.cdequantize_blockwise_cpu_fp32(get_ptr(code), get_ptr(Ac), get_ptr(absmax), get_ptr(o32),
                                            ct.c_longlong(quant_state.blocksize), ct.c_longlong(A.numel()))
         if o32 is not out:
             out.copy_(o32)
@@ -738,22 +740,28 @@ GEMM_4BIT_WIDE_MAX_ROWS = 256
 # once and dotted with each row, whole K per workgroup, one launch, rows bit-identical to gemv_4bit on each row).
 GEMM_4BIT_GEMV_TOKENS = 4
 
-# Measured route for prefill shapes (more than GEMM_4BIT_FEW_TOKENS rows).  The static rule above is a coarse map and
-# the libraries' own solution choice can be far off: torch's default hipBLASLt heuristic runs 4096 x 11008 x 4096
-# (rows x out x in: the gate/up projection at 4096 tokens) at 0.9 PFLOP/s, where the fused kernel reaches 1.06 and a
-# searched rocBLAS solution 1.45; at 1536 rows the fused kernel's 258 tiles take two passes over 256 CUs and the pair
-# is 1.5-1.7x faster (profiles/lab/r02_lib_route.txt, r02_rocblas_solutions.txt, r02_mid_rows_route.txt).  So the
-# first call of a shape (per device, dtype and statistics format) times three routes on its own operands (one warm
-# call each, then the best of three interleaved rounds): "library" (dequantise + torch.matmul, torch's hipBLASLt heuristic), "library_tn"
-# (dequantise + cgemm_tn_*, rocBLAS with the per-shape solution search of gemm_lib.hip) and "fused" (the hand-written
-# kernel), and leaves the static rule's route only for one faster by more than GEMM_4BIT_ROUTE_MARGIN; during
-# HIP-graph capture nothing is timed and the static rule stands.  The choice is cached
-# for the process per quarter-octave bucket of the row count (_route_rows_bucket).  The first call of a bucket costs
-# about a second (the rocBLAS solution search included).  GEMM_4BIT_ROUTE_TUNING = False (or BNB_ROUTE_TUNING=0 in
-# the environment): static rule only.
-GEMM_4BIT_ROUTE_TUNING = os.environ.get("BNB_ROUTE_TUNING", "1") != "0"
+# The large-prefill GEMM after the dequantise is the hand-written k_hgemm (hgemm.hip, chgemm_tn_*: 256 x 256 tiles,
+# 4 waves x 128 x 128 on v_mfma_f32_16x16x32) wherever its tile grid fills the chip (at least HGEMM_MIN_TILES tiles
+# of 256 x 256); smaller grids keep the library GEMM (torch.matmul).  4096 x 4096 x 11008: 229-231 us (1.60 PFLOP/s)
+# against rocBLAS's 215-217 us on the same box (profiles/lab/r03_hgemm_variants.txt).
+HGEMM_MIN_TILES = 192
+
+# Routing is deterministic by default: the static rule above picks the kernel from the shape alone, so every process
+# and every rank runs the same kernels on the same shape and returns the same bits.  BNB_ROUTE_TUNING=1 (or
+# GEMM_4BIT_ROUTE_TUNING = True) measures instead: the first call of a prefill shape (more than GEMM_4BIT_FEW_TOKENS
+# rows; per device, dtype and statistics format) times "hgemm" (dequantise + k_hgemm), "library" (dequantise +
+# torch.matmul), "library_tn" (dequantise + cgemm_tn_*, rocBLAS with the per-shape solution search of gemm_lib.hip)
+# and "fused" (the one-kernel NF4 GEMM) on its own operands (one warm call each, then the best of three interleaved
+# rounds) and leaves the static rule's route only for one faster by more than GEMM_4BIT_ROUTE_MARGIN; nothing is timed
+# during HIP-graph capture.  Choices are cached per quarter-octave bucket of the row count (_route_rows_bucket) and,
+# with BNB_ROUTE_PLAN=<file>, persisted as JSON and read back by later processes (and by every rank of a job that
+# shares the file), so a measured route is reproducible across processes too.  export_routes() / import_routes()
+# hand the table over explicitly (e.g. broadcast from rank 0).
+GEMM_4BIT_ROUTE_TUNING = os.environ.get("BNB_ROUTE_TUNING", "0") == "1"
 GEMM_4BIT_ROUTE_MARGIN = 0.05
+GEMM_4BIT_ROUTES = ("hgemm", "library", "library_tn", "fused")
 _ROUTES: dict = {}
+_ROUTE_PLAN_LOADED = [False]
 
 _DEQ_WS: dict = {}
 _DEQ_META: dict = {}
@@ -766,42 +774,127 @@ def _route_rows_bucket(rows: int) -> int:
     return rows // step * step
 
 
+@functools.lru_cache(maxsize=None)
+def _device_name(index: int) -> str:
+    try:
+        return torch.cuda.get_device_name(index)
+    except Exception:  # noqa: BLE001
+        return "unknown"
+
+
 def _route_key(A2: Tensor, state: QuantState, absmax: Optional[Tensor]):
-    return (A2.device.index, _route_rows_bucket(A2.shape[0]), state.shape[0], state.shape[1], A2.dtype,
-            state.quant_type, state.blocksize, state.nested and absmax is None)
+    # the device's NAME (not its index): a plan file measured on one MI355X applies to every MI355X of the job
+    return (_device_name(A2.device.index), _route_rows_bucket(A2.shape[0]), state.shape[0], state.shape[1],
+            str(A2.dtype), state.quant_type, state.blocksize, bool(state.nested and absmax is None))
+
+
+def _plan_path() -> Optional[str]:
+    return os.environ.get("BNB_ROUTE_PLAN") or None
+
+
+def _load_route_plan():
+    if _ROUTE_PLAN_LOADED[0]:
+        return
+    _ROUTE_PLAN_LOADED[0] = True
+    path = _plan_path()
+    if path and os.path.exists(path):
+        import json
+        with open(path) as f:
+            import_routes(json.load(f))
+
+
+def _save_route_plan():
+    path = _plan_path()
+    if not path:
+        return
+    import json
+    import tempfile
+    d = os.path.dirname(os.path.abspath(path))
+    fd, tmp = tempfile.mkstemp(dir=d, prefix=".route_plan")
+    with os.fdopen(fd, "w") as f:
+        json.dump(export_routes(), f, indent=1)
+    os.replace(tmp, path)   # atomic: a concurrent reader sees the old or the new table, never half of one
+
+
+def export_routes() -> dict:
+    """The measured route table as JSON-able data: {"version": 1, "routes": [[key..., route], ...]}."""
+    return {"version": 1, "routes": [list(k) + [r] for k, r in sorted(_ROUTES.items(), key=lambda kv: str(kv[0]))]}
+
+
+def import_routes(table: dict) -> int:
+    """Merge a table from export_routes() (entries naming an unknown route are ignored); returns the entry count."""
+    n = 0
+    for row in table.get("routes", []):
+        *key, route = row
+        if route in GEMM_4BIT_ROUTES and len(key) == 8:
+            _ROUTES[tuple(key)] = route
+            n += 1
+    return n
 
 
 def gemm_4bit_measured_route(A: Tensor, state: QuantState, absmax: Optional[Tensor] = None) -> Optional[str]:
-    """The measured route ("library" / "library_tn" / "fused") cached for A's rows against this weight, or None when
-    the shape has not been measured (the static rule applies)."""
+    """The measured route cached for A's rows against this weight, or None when the shape has not been measured (the
+    static rule applies)."""
+    _load_route_plan()
     return _ROUTES.get(_route_key(A.reshape(-1, state.shape[1]), state, absmax))
+
+
+def _hgemm_fits(rows: int, N: int, K: int) -> bool:
+    """chgemm_tn's own rule (k % 64, 32-bit lane offsets) plus a tile grid that fills the chip."""
+    tiles = ((rows + 255) // 256) * ((N + 255) // 256)
+    return (K % 64 == 0 and tiles >= HGEMM_MIN_TILES and (rows - 1) * K * 2 + 2 * K <= 0xFFFFFFFF
+            and (N - 1) * K * 2 + 2 * K <= 0xFFFFFFFF)
+
+
+def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
+    """The deterministic route of a (rows, N, K) product: "hgemm" / "library" for large prefill, else "fused" (the
+    few-token kernels and the multi-row GEMV are picked inside the fused branch)."""
+    if rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES:
+        return "hgemm" if _hgemm_fits(rows, N, K) else "library"
+    if GEMM_4BIT_FEW_TOKENS < rows <= GEMM_4BIT_WIDE_MAX_ROWS and N >= 2 * K:
+        return "library"
+    return "fused"
 
 
 def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor],
                  default: str) -> str:
-    """The measured route of a prefill shape: "library", "library_tn" or "fused" (see above); `default` is the static
-    rule's route, kept unless another is faster by more than GEMM_4BIT_ROUTE_MARGIN."""
+    """The measured route of a prefill shape (see above); `default` is the static rule's route, kept unless another
+    is faster by more than GEMM_4BIT_ROUTE_MARGIN.  Timed on A2's device and its current stream."""
+    _load_route_plan()
     key = _route_key(A2, state, absmax)
     route = _ROUTES.get(key)
     if route is not None:
         return route
-    if torch.cuda.is_current_stream_capturing():
-        return default
-    names = ("library", "library_tn", "fused")
-    for name in names:          # untimed: code-object loads, the rocBLAS solution search, workspaces, clock ramp
-        gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
-    times = {name: float("inf") for name in names}
-    for _ in range(3):          # interleaved rounds, best per route (no route is timed only on a colder clock)
-        for name in names:
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
+    with torch.cuda.device(A2.device):
+        stream = torch.cuda.current_stream(A2.device)
+        if torch.cuda.is_current_stream_capturing():
+            return default
+        ws_key = (A2.device, A2.dtype, _stream_key(A2.device))
+        ws_before = _DEQ_WS.get(ws_key)
+        rows, N, K = A2.shape[0], state.shape[0], state.shape[1]
+        names = [n for n in GEMM_4BIT_ROUTES if n != "hgemm" or _hgemm_fits(rows, N, K)]
+        for name in names:      # untimed: code-object loads, the rocBLAS solution search, workspaces, clock ramp
             gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
-            e.record()
-            e.synchronize()
-            times[name] = min(times[name], s.elapsed_time(e))
-    fastest = min(times, key=times.get)
-    route = fastest if times[fastest] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times[default] else default
+        times = {name: float("inf") for name in names}
+        for _ in range(3):      # interleaved rounds, best per route (no route is timed only on a colder clock)
+            for name in names:
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record(stream)
+                gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
+                e.record(stream)
+                e.synchronize()
+                times[name] = min(times[name], s.elapsed_time(e))
+        fastest = min(times, key=times.get)
+        route = fastest if times[fastest] < (1.0 - GEMM_4BIT_ROUTE_MARGIN) * times.get(default, float("inf")) else default
+        if route == "fused" and _DEQ_WS.get(ws_key) is not ws_before:
+            # the library candidates grew the weight workspace for this measurement only: give it back
+            if ws_before is None:
+                _DEQ_WS.pop(ws_key, None)
+            else:
+                _DEQ_WS[ws_key] = ws_before
+            _DEQ_META.pop(ws_key, None)
     _ROUTES[key] = route
+    _save_route_plan()
     return route
 
 
@@ -862,7 +955,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     the caller runs several row chunks of one product against the same, unmodified weight (the chunked
     sharded forward); on the library path the workspace still holding this weight's dequantisation
     from the previous call is used as is.  Prefill shapes on the library side of the static rule take the
-    measured route (GEMM_4BIT_ROUTE_TUNING); _route ("library" / "library_tn" / "fused") forces one (internal)."""
+    measured route (GEMM_4BIT_ROUTE_TUNING); _route (one of GEMM_4BIT_ROUTES) forces one (internal)."""
     if not gemm_4bit_supported(A, state):
         raise ValueError("gemm_4bit: needs bf16/fp16 activations and in_features % 64 == 0")
     N, K = state.shape[0], state.shape[1]
@@ -870,17 +963,21 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if not A2.is_contiguous() or A2.data_ptr() % 16:
         A2 = A2.contiguous()
     rows = A2.shape[0]
-    library = ((rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES)
-               or (GEMM_4BIT_FEW_TOKENS < rows <= GEMM_4BIT_WIDE_MAX_ROWS and N >= 2 * K))
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
-    route = "library" if library else "fused"
+    route = gemm_4bit_static_route(rows, N, K)
     if _route is not None:
+        if _route not in GEMM_4BIT_ROUTES:
+            raise ValueError(f"gemm_4bit: unknown route {_route!r}")
         route = _route
     elif GEMM_4BIT_ROUTE_TUNING and rows > GEMM_4BIT_FEW_TOKENS:
         route = _tuned_route(A2, Bc, state, out.view(rows, N), absmax, route)
-    library = route in ("library", "library_tn")
+    elif rows > GEMM_4BIT_FEW_TOKENS and (_ROUTES or _plan_path()):
+        measured = gemm_4bit_measured_route(A2, state, absmax)   # a table handed over by import_routes / the plan file
+        if measured is not None:
+            route = measured
+    library = route in ("library", "library_tn", "hgemm")
     if not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events):
         return out.view(*A.shape[:-1], N)
     if (absmax is None and not library and rows <= GEMM_4BIT_FEW_TOKENS and _nested_stats_in_kernel_ok(state)):
@@ -935,7 +1032,16 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
                 events.append(("dequantize", ev[0], ev[1]))
         elif ev:
             ev[1].record()
-        if route == "library_tn":
+        if route == "hgemm":
+            # the hand-written GEMM (hgemm.hip)
+            fn = lib.chgemm_tn_bf16 if A.dtype == torch.bfloat16 else lib.chgemm_tn_fp16
+            rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W),
+                    ct.c_int32(K), get_ptr(out), ct.c_int32(N))
+            post_call(prev_device)
+            if rc:
+                raise RuntimeError(f"bitsandbytes HIP GEMM (chgemm_tn) returned {rc}: "
+                                   f"{lib.cget_last_error_message().decode() if rc == 2 else 'shape not supported'}")
+        elif route == "library_tn":
             # the library GEMM with the per-shape solution search (gemm_lib.hip, rocBLAS)
             fn = lib.cgemm_tn_bf16 if A.dtype == torch.bfloat16 else lib.cgemm_tn_fp16
             rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W),

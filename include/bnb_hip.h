@@ -205,6 +205,12 @@ int cgemm_tn_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp1
  * 1 = fp16): 1 = a searched rocBLAS solution, 0 = the standard algorithm, -1 = not searched yet. */
 int cgemm_tn_set_search(int on, double budget_ms, int clear);
 int cgemm_tn_plan(int m, int n, int k, int dtype, int lda, int ldw, int ldc);
+/* [additive] the same product on the hand-written gfx950 GEMM (hgemm.hip: 256 x 256 tile, 4 waves x 128 x 128 on
+ * v_mfma_f32_16x16x32, both operands by LDS-DMA): the large-prefill route of the 4-bit path after the dequantise
+ * (ref:autograd/_functions.py:507's F.linear).  Returns 0 = launched, 1 = shape not supported (k % 64 != 0, rows not
+ * 16-B aligned; nothing launched), 2 = launch error (cget_last_error*). */
+int chgemm_tn_bf16(int m, int n, int k, const bnb_bf16* A, int lda, const bnb_bf16* W, int ldw, bnb_bf16* C, int ldc);
+int chgemm_tn_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp16* W, int ldw, bnb_fp16* C, int ldc);
 /* [additive, testing] int8 split-K factor: -1 = auto, 1 = never, >= 2 = force where it applies */
 void cigemm_set_splitk(int ks);
 /* [additive, testing] force the int8 GEMM tile kernel: 0 = auto (256x256 when it applies), 128 = 128x128 */

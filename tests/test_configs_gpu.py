@@ -3,7 +3,8 @@
 * Metric shape (M=4096, N=4096, K=11008, NF4 bs=64, nested statistics): functional.gemm_4bit as routed (and the
   fused kernel forced), against the fp64 oracle ref.gemm_4bit_dequant_ref (the reference's M > 1 algorithm,
   ref:autograd/_functions.py:491-507) on 256 sampled rows x all columns.
-* Config 4: the three distinct Llama-2-7B projection shapes (4096x4096, 11008x4096, 4096x11008) at 2048 tokens.
+* Config 4: the three distinct Llama-2-7B projection shapes (4096x4096, 11008x4096, 4096x11008) at 2048 tokens and
+  at the config's own 65,536 tokens (batch 32 x seq 2048).
 * Config 5: one 8-way column shard of each Llama-2-70B projection (q/o 8192x8192, k/v 1024x8192,
   gate/up 28672x8192, down 8192x28672, each N/8) at 2048 tokens, from a full-size quantised weight sliced by
   parallel.shard_quantized_4bit (packed bytes, uint8 codes and second-level scales sliced: every 70B shard starts
@@ -49,17 +50,35 @@ def _quantized(N, K, dev, seed):
     return q, st
 
 
-@pytest.mark.parametrize("route", ["routed", "fused"])
-def test_metric_shape(dev, route, monkeypatch):
+@pytest.mark.parametrize("route", ["routed", "hgemm", "fused"])
+def test_metric_shape(dev, route):
+    """The metric shape as routed (deterministic rule: dequantise + the hand-written k_hgemm), with k_hgemm forced,
+    and with the one-kernel fused NF4 GEMM forced."""
     F = _F()
     M, N, K = 4096, 4096, 11008
     q, st = _quantized(N, K, dev, 1000)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=torch.Generator(device=dev).manual_seed(1))
-    if route == "fused":
-        monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1 << 30)
-        monkeypatch.setattr(F, "GEMM_4BIT_ROUTE_TUNING", False)
-    Y = F.gemm_4bit(X, q, st)
+    if route == "routed":
+        assert F.gemm_4bit_static_route(M, N, K) == "hgemm"
+        Y = F.gemm_4bit(X, q, st)
+    else:
+        Y = F.gemm_4bit(X, q, st, _route=route)
     _check_rows(Y, X, q, F._absmax_fp32(st), N, K, st.code, _sample_rows(M, dev))
+
+
+@pytest.mark.parametrize("n_out,k_in", [(4096, 4096), (11008, 4096), (4096, 11008)])
+def test_llama2_7b_prefill_65536_tokens(dev, n_out, k_in):
+    """Config 4 at its own size: batch 32 x seq 2048 = 65,536 activation rows through each distinct Llama-2-7B
+    projection shape, on the route the product takes there (k_hgemm), 256 sampled rows against the fp64 oracle."""
+    F = _F()
+    M = 65536
+    assert F.gemm_4bit_static_route(M, n_out, k_in) == "hgemm"
+    q, st = _quantized(n_out, k_in, dev, 7 * n_out + k_in)
+    X = torch.randn(M, k_in, device=dev, dtype=torch.bfloat16,
+                    generator=torch.Generator(device=dev).manual_seed(n_out - k_in))
+    Y = F.gemm_4bit(X, q, st)
+    assert Y.shape == (M, n_out)
+    _check_rows(Y, X, q, F._absmax_fp32(st), n_out, k_in, st.code, _sample_rows(M, dev, seed=n_out // 3))
 
 
 @pytest.mark.parametrize("n_out,k_in", [(4096, 4096), (11008, 4096), (4096, 11008)])
@@ -96,30 +115,39 @@ def test_llama2_70b_shard(dev, name, n_out, k_in):
     assert torch.equal(qs.reshape(-1), q.reshape(-1)[rank * n * k_in // 2:(rank + 1) * n * k_in // 2])
 
 
-def test_measured_route_4096_tokens_gate_up(dev):
-    """The gate/up projection at 4096 tokens (11008 x 4096 weight), where torch's default hipBLASLt solution is
-    slow: the first call measures the three routes (functional.GEMM_4BIT_ROUTE_TUNING: torch's library GEMM, the
-    rocBLAS-searched one, the fused kernel) and caches one; every forced route and the routed call are within the
-    oracle tolerance, the cache is stable, and a call under HIP-graph capture neither measures nor fails."""
+def test_measured_route_4096_tokens_gate_up(dev, monkeypatch, tmp_path):
+    """BNB_ROUTE_TUNING mode on the gate/up projection at 4096 tokens (11008 x 4096 weight): the first call times the
+    four routes (k_hgemm, torch's library GEMM, the rocBLAS-searched one, the fused kernel) and caches one; every forced
+    route and the routed call are within the oracle tolerance, the cache is stable, the plan file holds the choice and
+    a process that imports it routes the same way, and a call under HIP-graph capture neither measures nor fails."""
     F = _F()
+    monkeypatch.setattr(F, "GEMM_4BIT_ROUTE_TUNING", True)
+    plan = tmp_path / "plan.json"
+    monkeypatch.setenv("BNB_ROUTE_PLAN", str(plan))
+    monkeypatch.setattr(F, "_ROUTES", {})
+    monkeypatch.setattr(F, "_ROUTE_PLAN_LOADED", [True])
     M, N, K = 4096, 11008, 4096
     q, st = _quantized(N, K, dev, 77)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=torch.Generator(device=dev).manual_seed(7))
     rows = _sample_rows(M, dev, n=128, seed=3)
     am = F._absmax_fp32(st)
-    F._ROUTES.pop(F._route_key(X, st, None), None)
-    for route in ("library", "library_tn", "fused"):
+    for route in F.GEMM_4BIT_ROUTES:
         Y = F.gemm_4bit(X, q, st, _route=route)
         _check_rows(Y, X, q, am, N, K, st.code, rows)
     Y = F.gemm_4bit(X, q, st)
     first = F.gemm_4bit_measured_route(X, st)
-    assert first in ("library", "library_tn", "fused")
+    assert first in F.GEMM_4BIT_ROUTES
     _check_rows(Y, X, q, am, N, K, st.code, rows)
     F.gemm_4bit(X, q, st)
     assert F.gemm_4bit_measured_route(X, st) == first
+    # the plan file: a fresh table (another process) imports the same choice
+    import json
+    table = json.loads(plan.read_text())
+    assert [r[-1] for r in table["routes"]] == [first]
+    monkeypatch.setattr(F, "_ROUTES", {})
+    assert F.import_routes(table) == 1 and F.gemm_4bit_measured_route(X, st) == first
     # capture: an unmeasured shape takes the static rule without timing anything
     X2 = X[:3072].contiguous()
-    F._ROUTES.pop(F._route_key(X2, st, None), None)
     out = torch.empty(3072, N, device=dev, dtype=torch.bfloat16)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -135,3 +163,35 @@ def test_measured_route_4096_tokens_gate_up(dev):
     g.replay()
     torch.cuda.synchronize()
     _check_rows(out, X2, q, am, N, K, st.code, rows[rows < 3072])
+
+
+_REPRO_SCRIPT = r"""
+import hashlib, sys, torch
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/bitsandbytes-sycl_amd"]
+import python_src_quants.functional as F
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev).manual_seed(1000)
+W = (torch.randn(4096, 11008, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+X = torch.randn(4096, 11008, device=dev, dtype=torch.bfloat16, generator=torch.Generator(device=dev).manual_seed(1))
+Y = F.gemm_4bit(X, q, st)
+torch.cuda.synchronize()
+print("DIGEST", hashlib.sha256(Y.view(torch.int16).cpu().numpy().tobytes()).hexdigest())
+"""
+
+
+def test_metric_shape_bits_reproducible_across_processes(dev):
+    """Two fresh processes (default, deterministic routing) compute the metric-shape product and return the same
+    bits: the route does not depend on per-process timing."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("BNB_ROUTE_TUNING", "BNB_ROUTE_PLAN")}
+    digests = []
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-c", _REPRO_SCRIPT, root], capture_output=True, text=True, env=env,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        digests.append([ln for ln in r.stdout.splitlines() if ln.startswith("DIGEST")][0])
+    assert digests[0] == digests[1]

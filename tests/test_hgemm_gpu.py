@@ -1,0 +1,134 @@
+"""The hand-written gfx950 GEMM behind the large-prefill 4-bit route (csrc/hgemm.hip, C-ABI chgemm_tn_*): the
+F.linear of ref:python_src_quants/autograd/_functions.py:507 after the dequantise, C[m, n] = A[m, k] . W[n, k]^T.
+
+Floating-point contract (a floating-point kernel, so the check is against a plain torch fp32 product of the same
+operands): fp32 accumulation, one RNE rounding to bf16 / fp16 at the end -- |C - C32| <= 2^-8 |C32| (bf16) or
+2^-11 |C32| (fp16) plus 1e-4 of the output rms for the accumulation-order difference.  Plus: deterministic (same bits
+on every call), edge tiles (ragged m, n), the unsupported-shape return code, HIP-graph replay, and the gemm_4bit
+"hgemm" route against the oracle."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _F():
+    import python_src_quants.functional as F
+    return F
+
+
+def _hgemm(F, X, W, out=None, lda=None, ldw=None):
+    m, k = X.shape
+    n = W.shape[0]
+    if out is None:
+        out = torch.empty(m, n, device=X.device, dtype=X.dtype)
+    fn = F.lib.chgemm_tn_bf16 if X.dtype == torch.bfloat16 else F.lib.chgemm_tn_fp16
+    F.pre_call(X.device)
+    rc = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(X), ct.c_int32(lda or X.stride(0)), F.get_ptr(W),
+            ct.c_int32(ldw or W.stride(0)), F.get_ptr(out), ct.c_int32(out.stride(0)))
+    return rc, out
+
+
+def _check(Y, X, W):
+    exp = torch.matmul(X.float(), W.float().t())
+    rel = 2.0 ** -8 if Y.dtype == torch.bfloat16 else 2.0 ** -11
+    err = (Y.float() - exp).abs()
+    bound = rel * exp.abs() + 1e-4 * exp.pow(2).mean().sqrt()
+    bad = (err > bound).sum().item()
+    assert bad == 0, (bad, err.max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mnk", [(4096, 4096, 11008), (1000, 1100, 4096), (257, 513, 64), (4096, 11008, 4096),
+                                 (3, 5, 128), (512, 256, 28672)])
+def test_hgemm_against_fp32_product(dev, dtype, mnk):
+    F = _F()
+    m, n, k = mnk
+    g = torch.Generator(device=dev).manual_seed(m * 7 + n)
+    X = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    W = (torch.rand(n, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    rc, Y = _hgemm(F, X, W)
+    torch.cuda.synchronize()
+    assert rc == 0
+    _check(Y, X, W)
+    rc2, Y2 = _hgemm(F, X, W)
+    torch.cuda.synchronize()
+    assert rc2 == 0 and torch.equal(Y, Y2)          # deterministic
+
+
+def test_hgemm_strided_operands_and_output(dev):
+    """Leading dimensions larger than k / n (row slices of wider buffers), output written into a strided view."""
+    F = _F()
+    m, n, k = 600, 700, 1024
+    g = torch.Generator(device=dev).manual_seed(5)
+    Xb = torch.randn(m, k + 64, device=dev, generator=g).to(torch.bfloat16)
+    Wb = torch.randn(n, k + 128, device=dev, generator=g).to(torch.bfloat16)
+    X, W = Xb[:, :k], Wb[:, :k]
+    Ob = torch.full((m, n + 8), 7.0, device=dev, dtype=torch.bfloat16)
+    rc, _ = _hgemm(F, X, W, out=Ob[:, :n], lda=k + 64, ldw=k + 128)
+    torch.cuda.synchronize()
+    assert rc == 0
+    _check(Ob[:, :n], X, W)
+    assert torch.all(Ob[:, n:] == 7.0)              # nothing written past n
+
+
+def test_hgemm_declines_unsupported_shapes(dev):
+    F = _F()
+    X = torch.randn(256, 96, device=dev, dtype=torch.bfloat16)
+    W = torch.randn(256, 96, device=dev, dtype=torch.bfloat16)
+    rc, _ = _hgemm(F, X, W)                          # k % 64 != 0
+    assert rc == 1
+    X = torch.randn(256, 132, device=dev, dtype=torch.bfloat16)
+    W = torch.randn(256, 132, device=dev, dtype=torch.bfloat16)
+    rc, _ = _hgemm(F, X[:, :128], W[:, :128], lda=132, ldw=132)   # rows not 16-B aligned
+    assert rc == 1
+
+
+def test_hgemm_graph_replay(dev):
+    F = _F()
+    m, n, k = 2048, 2048, 2048
+    X = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    W = torch.randn(n, k, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    _hgemm(F, X, W, out=out)
+    ref_out = out.clone()
+    out.zero_()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            _hgemm(F, X, W, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref_out)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+def test_gemm_4bit_hgemm_route_vs_oracle(dev, dtype, nested):
+    """gemm_4bit's "hgemm" route (dequantise into the weight workspace + k_hgemm) within the GEMM tolerance of the fp64
+    oracle (the reference's M > 1 algorithm, ref:autograd/_functions.py:491-507), and equal to the dequantised weight
+    multiplied by chgemm_tn directly."""
+    F = _F()
+    M, N, K = 1024, 1536, 2048
+    torch.manual_seed(11 + nested)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    Y = F.gemm_4bit(X, q, st, _route="hgemm")
+    _, Yd = _hgemm(F, X, F.dequantize_4bit(q, st))
+    assert torch.equal(Y, Yd)
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64, st.code.cpu().numpy(),
+                                    "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    got = Y.float().cpu().numpy().astype(np.float64)
+    rms = np.sqrt(np.mean(exp ** 2))
+    assert np.all(np.abs(got - exp) <= tol * rms + tol * np.abs(exp))

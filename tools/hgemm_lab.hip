@@ -1,0 +1,106 @@
+// LAB (not built into the library): csrc/hgemm.hip (hand-written 4-wave 256x256 bf16 GEMM) against rocBLAS's
+// standard algorithm on the same operands: agreement (fp32-accumulated references, bf16 outputs) and timing,
+// interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).  Operands uniform [-1, 1) random.
+// Usage: hgemm_lab [M N K] [rounds]
+#define ROCBLAS_BETA_FEATURES_API
+#pragma clang diagnostic ignored "-Wdeprecated-declarations"
+#include <rocblas/rocblas.h>
+
+#include "hgemm.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace bnb {
+hipStream_t current_stream() { return nullptr; }
+void set_error(int, const char* what) { printf("error: %s\n", what); }
+int g_tile_override = 0;
+}  // namespace bnb
+using namespace bnb;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+static float bf2f(uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return f; }
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096, K = argc > 3 ? atoi(argv[3]) : 11008;
+  const int rounds = argc > 4 ? atoi(argv[4]) : 5;
+  uint16_t *X, *W, *Y0, *Y1;
+  CK(hipMalloc(&X, (size_t)M * K * 2)); CK(hipMalloc(&W, (size_t)N * K * 2));
+  CK(hipMalloc(&Y0, (size_t)M * N * 2)); CK(hipMalloc(&Y1, (size_t)M * N * 2));
+  {
+    std::vector<uint16_t> h((size_t)std::max(M, N) * K);
+    srand(3);
+    for (auto& v : h) { float f = ((rand() & 0xFFFF) - 32768) / 32768.0f; uint32_t u; memcpy(&u, &f, 4); v = (uint16_t)(u >> 16); }
+    CK(hipMemcpy(X, h.data(), (size_t)M * K * 2, hipMemcpyHostToDevice));
+    for (auto& v : h) { float f = ((rand() & 0xFFFF) - 32768) / 32768.0f; uint32_t u; memcpy(&u, &f, 4); v = (uint16_t)(u >> 16); }
+    CK(hipMemcpy(W, h.data(), (size_t)N * K * 2, hipMemcpyHostToDevice));
+  }
+  rocblas_handle h;
+  rocblas_create_handle(&h);
+  const float alpha = 1.0f, beta = 0.0f;
+  auto lib = [&]() {
+    rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &alpha, W, rocblas_datatype_bf16_r, K, X,
+                    rocblas_datatype_bf16_r, K, &beta, Y0, rocblas_datatype_bf16_r, N, Y0, rocblas_datatype_bf16_r, N,
+                    rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
+  };
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  auto mine = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(HG_THREADS), 0, 0, M, N, K, (const bf16_t*)X, (long long)K, (const bf16_t*)W,
+                       (long long)K, (bf16_t*)Y1, (long long)N);
+  };
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  auto timeit = [&](auto go, int R) {
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < R; ++i) go();
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1e3 / R;
+  };
+  auto agree = [&](const char* name) {
+    std::vector<uint16_t> a((size_t)M * N), b((size_t)M * N);
+    CK(hipMemcpy(a.data(), Y0, a.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), Y1, b.size() * 2, hipMemcpyDeviceToHost));
+    double maxd = 0, maxa = 0, sumd = 0;
+    size_t nbad = 0;
+    for (size_t i = 0; i < a.size(); ++i) {
+      const double x = bf2f(a[i]), y = bf2f(b[i]);
+      const double d = fabs(x - y);
+      maxd = fmax(maxd, d); maxa = fmax(maxa, fabs(x)); sumd += d;
+      if (!(d <= 0.01 * fabs(x) + 0.02 * sqrt((double)K / 3.0) * 0.05)) ++nbad;
+    }
+    printf("%-12s agreement: max|d| %.4g  max|ref| %.4g  mean|d| %.4g  bad %zu / %zu\n", name, maxd, maxa, sumd / a.size(), nbad,
+           a.size());
+  };
+  const double flop = 2.0 * M * N * K;
+  // warm the clocks on the library, then correctness, then interleaved rounds
+  for (int i = 0; i < 100; ++i) lib();
+  CK(hipDeviceSynchronize());
+  auto check = [&](auto kern, const char* name) {
+    CK(hipMemset(Y1, 0xFF, (size_t)M * N * 2));
+    mine(kern);
+    CK(hipDeviceSynchronize());
+    agree(name);
+  };
+  check(k_hgemm<bf16_t, 0>, "hgemm v0");
+  check(k_hgemm<bf16_t, 4>, "hgemm v4");
+  check(k_hgemm<bf16_t, 8>, "hgemm v8");
+  check(k_hgemm<bf16_t, 12>, "hgemm v12");
+  const int R = 20;
+  for (int r = 0; r < rounds; ++r) {
+    const double t_lib = timeit(lib, R);
+    double tv[4];
+    tv[0] = timeit([&] { mine(k_hgemm<bf16_t, 0>); }, R);
+    tv[1] = timeit([&] { mine(k_hgemm<bf16_t, 4>); }, R);
+    tv[2] = timeit([&] { mine(k_hgemm<bf16_t, 8>); }, R);
+    tv[3] = timeit([&] { mine(k_hgemm<bf16_t, 12>); }, R);
+    printf("round %d  rocblas %7.1f us %6.0f TF |", r, t_lib, flop / t_lib / 1e6);
+    for (int v = 0; v < 4; ++v) printf(" v%d %7.1f us %6.0f TF |", 4 * v, tv[v], flop / tv[v] / 1e6);
+    printf("\n");
+    fflush(stdout);
+  }
+  return 0;
+}
