@@ -173,6 +173,58 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
             "frac_of_int8_peak": ops / per / 1e12 / PEAK_INT8_TOPS}
 
 
+def bench_decode_sharded(dev, world, rank, steps, warmup):
+    """Decode (M = 1) on `world` GPUs: the config-2 weight (Linear4bit NF4 11008 x 4096, nested statistics) sharded by
+    output feature (ColumnShardedLinear4bit.from_quantized), one step = this rank's GEMV + ONE RCCL all-gather of the
+    [1, 11008/world] bf16 shard outputs + the [1, 11008] row assembled (parallel.ShardedDecode, static buffers),
+    captured in one HIP graph and replayed.  At M = 1 the all-gather moves KB and is latency-bound, so
+    this reports latency: us per token for the layer, max over ranks, barrier-bracketed like the main step.  Ranks
+    agree on the capture (all must succeed, else every rank replays the same step eagerly)."""
+    from python_src_quants.parallel import ColumnShardedLinear4bit
+    n_out, k_in = 11008, 4096
+    g = torch.Generator(device=dev).manual_seed(2)
+    W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True)
+    del W
+    lin = ColumnShardedLinear4bit.from_quantized(q, st, world, rank)
+    lin.qweight = lin.qweight.clone()
+    del q
+    dec = lin.decode_step()
+    dec.set_input(torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g))
+    graph = dec.capture()
+    if world > 1:
+        ok = torch.tensor([1 if graph else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() == 0:
+            dec.graph, graph = None, False
+    for _ in range(max(warmup, 3)):
+        dec()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dec()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    per = elapsed / steps
+    n = n_out // world
+    wbytes = n * k_in // 2 + n * k_in // BS + n * k_in // BS // 256 * 4 + 1024
+    return {"shape": [1, n_out, k_in], "n_gpus": world, "us_per_token": per * 1e6, "hip_graph": bool(graph),
+            "weight_bytes_per_rank": wbytes, "rank_weight_gbs": wbytes / per / 1e9,
+            "step": "gemv_4bit on this rank's rows" + (" + RCCL all_gather_into_tensor [1, N/g] + [1, N] assembly"
+                                                        if world > 1 else " + [1, N] copy"),
+            "note": "host wall per replayed step (barrier-bracketed, max over ranks): the latency a decode token pays"}
+
+
 def _time_graph(calls, iters):
     """Capture one pass over `calls` (distinct buffers each) into a HIP graph and time replays, so the
     number is the kernels' back-to-back time rather than the Python launch rate."""
@@ -494,16 +546,18 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
 
 
 def gemm_kernel_name(m, n, k=K, route=None):
-    """Which kernel carries gemm_4bit's flops for m tokens x n features: from GEMM_4BIT_DEQUANT_MIN_ROWS
-    tokens the library GEMM after the dequantise kernel (torch's hipBLASLt pick, or with route "library_tn" the
-    rocBLAS-searched one; unless the measured route, `route`, is "fused");
-    below, gemm4bit.hip's 256x256 tile kernel when the features are >= 256 and the grid (with split-K) has
-    >= 128 workgroups, else the 128x128 one."""
-    static_library = m >= F.GEMM_4BIT_DEQUANT_MIN_ROWS and n >= F.GEMM_4BIT_DEQUANT_MIN_FEATURES
-    if route in ("library", "library_tn") or (route is None and static_library):
-        if route == "library_tn":
-            return ("library bf16 GEMM (Cijk_*, rocBLAS solution searched per shape, cgemm_tn_bf16) after "
-                    "k_dequantize_4bit_stream<bf16,NF4>")
+    """Which kernel carries gemm_4bit's flops for m tokens x n features: the route (measured when `route` is given,
+    else functional.gemm_4bit_static_route) -- "hgemm": the hand-written k_hgemm after the dequantise kernel;
+    "library" / "library_tn": the library GEMM after the dequantise kernel (torch's hipBLASLt pick / the
+    rocBLAS-searched one); "fused": gemm4bit.hip's 256x256 tile kernel when the features are >= 256 and the grid (with
+    split-K) has >= 128 workgroups, else the 128x128 one."""
+    route = route or F.gemm_4bit_static_route(m, n, k)
+    if route == "hgemm":
+        return "k_hgemm<bf16> (hand-written, hgemm.hip) after k_dequantize_4bit_stream<bf16,NF4>"
+    if route == "library_tn":
+        return ("library bf16 GEMM (Cijk_*, rocBLAS solution searched per shape, cgemm_tn_bf16) after "
+                "k_dequantize_4bit_stream<bf16,NF4>")
+    if route == "library":
         return "library bf16 GEMM (Cijk_* hipBLASLt, via torch.matmul) after k_dequantize_4bit_stream<bf16,NF4>"
     ks = max(1, F.lib.cgemm_4bit_workspace_bytes(ct.c_int32(n), ct.c_int32(m), ct.c_int32(k)) // (4 * m * n))
     tiles256 = ((m + 255) // 256) * ((n + 255) // 256)
@@ -511,6 +565,61 @@ def gemm_kernel_name(m, n, k=K, route=None):
     if n >= 256 and (tiles256 * ks >= 128 or 2 * tiles256 * ks >= tiles128):
         return "k_gemm_4bit_256<bf16>" + (f" split-K x{ks} + k_splitk_reduce" if ks > 1 else "")
     return "k_gemm_4bit<bf16>"
+
+
+def dequant_route(kname):
+    """True when the kernel carrying the flops runs after the dequantise kernel (statistics decoded there)."""
+    return kname.startswith("library") or kname.startswith("k_hgemm")
+
+
+def measure_peaks(dev, reps=5):
+    """Measured ceilings on this box (spec AND measured peak), from the library's probe kernels
+    (csrc/probe.hip): the dense bf16 and int8 MFMA rate on random register operands at one wave per SIMD (the GEMMs'
+    own shapes and occupancy), and the HBM streaming read rate over 2 GiB (> the 256 MB MALL).  Median of `reps`
+    timed launches after a ~0.3 s clock ramp."""
+    import statistics
+    blocks = 256         # one workgroup per CU: 4 waves (one per SIMD) or 8 (two per SIMD)
+    sink = torch.empty(blocks * 512, device=dev)
+    res = {}
+    for kind, name, per in ((0, "bf16_mfma_tflops", 16 * 16 * 32 * 2), (1, "int8_mfma_tops", 16 * 16 * 64 * 2)):
+        best = {}
+        for waves in (4, 8):
+            k = kind + (2 if waves == 8 else 0)
+            iters = 40000
+            F.pre_call(dev)
+            t_end = time.perf_counter() + 0.3
+            while time.perf_counter() < t_end:
+                F.lib.cprobe_mfma(k, blocks, iters, 7, F.get_ptr(sink))
+                torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps):
+                s, e = _events()
+                s.record()
+                F.lib.cprobe_mfma(k, blocks, iters, 7, F.get_ptr(sink))
+                e.record()
+                e.synchronize()
+                ts.append(s.elapsed_time(e) * 1e-3)
+            best[waves] = blocks * waves * 8 * iters * per / statistics.median(ts) / 1e12
+        res[name] = max(best.values())
+        res[name + "_by_waves_per_cu"] = {str(w): round(v, 1) for w, v in best.items()}
+    buf = torch.empty(1 << 31, dtype=torch.uint8, device=dev)
+    hsink = torch.empty(4096, dtype=torch.int32, device=dev)
+    ts = []
+    for i in range(reps + 2):
+        s, e = _events()
+        s.record()
+        F.lib.cprobe_hbm_read(F.get_ptr(buf), ct.c_longlong(buf.numel()), 4096, F.get_ptr(hsink))
+        e.record()
+        e.synchronize()
+        if i >= 2:
+            ts.append(s.elapsed_time(e) * 1e-3)
+    res["hbm_read_gbs"] = buf.numel() / statistics.median(ts) / 1e9
+    del buf
+    torch.cuda.empty_cache()
+    res["how"] = ("csrc/probe.hip: MFMA 16x16x32 bf16 / 16x16x64 i8 back to back on random register operands, one or two "
+                  "waves per SIMD (the faster is the peak), 8 AGPR accumulators per wave; HBM: 16-B non-temporal loads, "
+                  "8 in flight per lane, 2 GiB buffer")
+    return res
 
 
 def load_pmc_traffic():
@@ -532,6 +641,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip int8/decode/config-1/cpu legs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-int8", action="store_true", help="skip the sharded int8 leg")
+    ap.add_argument("--no-decode", action="store_true", help="skip the sharded decode (M = 1) leg")
     ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 ranks on one GPU")
@@ -573,7 +683,7 @@ def main():
     full_out = torch.empty(M, world * shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
     kev = []
 
-    library = gemm_kernel_name(Mc, shard).startswith("library")
+    library = dequant_route(gemm_kernel_name(Mc, shard))
 
     clock = StepClock(args.steps)
 
@@ -601,8 +711,8 @@ def main():
     # clock ramp: MI355X takes ~0.1-0.3 s of sustained MFMA load to reach its steady clock; run the
     # step untimed for --prewarm-ms before the W counted warmup steps (the timed region is unchanged)
     # (GEMM only: a time-based loop must not contain a collective, ranks could disagree on its count)
-    # the first call of the shape measures its route (functional.GEMM_4BIT_ROUTE_TUNING; about a second with the
-    # library solution search): done before the clock-ramp period starts, so the ramp is not spent on it
+    # first call of the shape (workspaces; under BNB_ROUTE_TUNING its route measurement): done before the clock-ramp
+    # period starts, so the ramp is not spent on it
     F.gemm_4bit(X[:Mc], q, st, out=Y[:Mc], absmax=None if library else F._absmax_fp32(st))
     torch.cuda.synchronize()
     t_end = time.perf_counter() + args.prewarm_ms / 1e3
@@ -611,9 +721,9 @@ def main():
         for c in range(chunks):
             F.gemm_4bit(X[c * Mc:(c + 1) * Mc], q, st, out=Y[c * Mc:(c + 1) * Mc], absmax=am)
         torch.cuda.synchronize()
-    # the route gemm_4bit measured for this shape on its first call (functional.GEMM_4BIT_ROUTE_TUNING)
+    # the route gemm_4bit takes for this shape (the static rule, or a measured one under BNB_ROUTE_TUNING)
     kname = gemm_kernel_name(Mc, shard, route=F.gemm_4bit_measured_route(X[:Mc], st))
-    library = kname.startswith("library")
+    library = dequant_route(kname)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -652,6 +762,8 @@ def main():
     extras = {}
     if not args.no_int8:     # every rank: it contains collectives when world > 1
         extras["int8_igemmlt_sharded"] = bench_int8_sharded(dev, world, rank, args.steps, args.warmup, chunks)
+    if not args.no_decode:   # every rank: the sharded decode step (GEMV + all-gather) as one HIP graph
+        extras["decode_sharded_config2"] = bench_decode_sharded(dev, world, rank, args.steps, args.warmup)
     if rank == 0 and world == 1 and not args.no_extras:
         extras["int8_igemmlt_metric_shape"] = bench_int8(dev, M, N, K)
         extras["int8_igemmlt_config3"] = bench_int8(dev, 4096, 4096, 4096)
@@ -662,6 +774,12 @@ def main():
         extras["nf4_fused_kernel_metric_shape"] = bench_nf4_fused_kernel(dev)
         extras["llama2_7b_prefill_config4"] = bench_llama2_7b_prefill(dev)
         extras["llama2_70b_rank_shard_config5"] = bench_llama2_70b_shard(dev)
+    peaks = None
+    if rank == 0 and not args.no_extras:
+        try:
+            peaks = measure_peaks(dev)
+        except Exception as ex:  # noqa: BLE001
+            peaks = {"error": str(ex)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.no_extras:
         try:
@@ -669,6 +787,10 @@ def main():
         except Exception as ex:  # noqa: BLE001
             cpu = {"value": None, "unit": "TFLOP/s", "cores": None, "kind": "port", "sample": f"failed: {ex}"}
 
+    if rank == 0 and peaks and "int8_mfma_tops" in peaks:
+        for key in ("int8_igemmlt_sharded", "int8_igemmlt_metric_shape", "int8_igemmlt_config3"):
+            if key in extras and "tops" in extras[key]:
+                extras[key]["frac_of_int8_peak_measured"] = extras[key]["tops"] / peaks["int8_mfma_tops"]
     if rank == 0:
         pmc = load_pmc_traffic()
         traffic = None
@@ -691,17 +813,24 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (seeded randn; W ~ N(0,0.02) -> NF4 bs=64 nested stats; X ~ N(0,1) bf16)",
             "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (functional.gemm_4bit: HIP "
-                                   "dequantise + hipBLASLt bf16 GEMM at this M; fused dequant+MFMA kernel below "
-                                   f"{F.GEMM_4BIT_DEQUANT_MIN_ROWS} rows / {F.GEMM_4BIT_DEQUANT_MIN_FEATURES} features) + bf16 all-gather of output-column shards",
+                                   "dequantise + the hand-written bf16 GEMM k_hgemm at this M; fused dequant+MFMA "
+                                   f"kernel below {F.GEMM_4BIT_DEQUANT_MIN_ROWS} rows / "
+                                   f"{F.GEMM_4BIT_DEQUANT_MIN_FEATURES} features) + bf16 all-gather of output-column "
+                                   "shards",
                        "M": M, "N": N, "K": K, "blocksize": BS, "quant_type": "nf4", "compress_statistics": True,
                        "parallelism": (f"column-shard x{world} + RCCL all_gather, {chunks} token-row chunks "
                                        "(chunk c's all-gather overlaps chunk c+1's GEMM; the step ends with the [M, N] "
                                        "output assembled)") if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                         "peak_measured": round(peaks["bf16_mfma_tflops"], 1) if peaks and "bf16_mfma_tflops" in peaks
+                         else None,
+                         "frac_measured": round(achieved / peaks["bf16_mfma_tflops"], 4)
+                         if peaks and "bf16_mfma_tflops" in peaks else None,
                          "kernel": kname, "kernel_us": round(kern_s * 1e6, 2),
                          "flops_per_launch": shard_flops,
                          "dequantize_us": round(deq_s * 1e6, 2) if deq_s else None, **pmc_extra},
+            "measured_peaks": peaks,
             "cpu_baseline": cpu,
         }
         line.update(extras)

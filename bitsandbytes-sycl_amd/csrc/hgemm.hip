@@ -20,6 +20,7 @@
 // The DMA of a tile is therefore in flight for a whole k-tile (~2k MFMA cycles), and no vmcnt(0) drain sits in
 // the loop (cdna_hip_programming.md §5 'Pipelining across barriers').
 #include "gemm_common.hpp"
+#include "int8_common.hpp"
 
 #include <type_traits>
 
@@ -28,7 +29,12 @@ namespace bnb {
 constexpr int HG_BM = 256, HG_BN = 256, HG_BK = 64, HG_THREADS = 256;
 constexpr int HG_TILE = HG_BM * HG_BK * 2;        // 32 KiB per operand per stage
 constexpr int HG_STAGE = 2 * HG_TILE;             // A + B
-constexpr int HG_LDS = 2 * HG_STAGE;              // 128 KiB
+constexpr int HG_LDS_MAIN = 2 * HG_STAGE;         // 128 KiB
+// epilogue staging of 16-bit outputs: per wave 128 rows x 256 B, rows padded to 272 B (16-B aligned; the 8-B
+// fragment writes of 16 consecutive rows then hit 2 banks each, 2-way at most)
+constexpr int HG_EPI_PITCH = 272;
+constexpr int HG_LDS_EPI = 4 * 128 * HG_EPI_PITCH;   // 136 KiB
+constexpr int HG_LDS = HG_LDS_MAIN > HG_LDS_EPI ? HG_LDS_MAIN : HG_LDS_EPI;
 
 // LDS-DMA with a scalar base: lane address = sbase + voff (unsigned 32-bit), 16 B per lane to lds + 16 * lane.
 // M0 (the LDS destination) is written and restored inside the statement (it is compiler-reserved).
@@ -52,50 +58,91 @@ template <> __device__ __forceinline__ uint32_t cvt_pk<fp16_t>(float lo, float h
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((hg_f32x2_t){lo, hi}, hg_f16x2_t));
 }
 
-// MFMA operand type kept native end to end (no uint4 <-> bf16x8 bit casts in the k-loop)
 // The MFMA is issued from inline asm with the accumulator pinned to AGPRs ("+a") and the fragments to VGPRs ("v"):
 // with the builtin, hipcc's allocator treats both as either-file operands and, at 256 accumulator registers, shuffles
 // them between the files every iteration (v_accvgpr_read/write/mov).  What the asm hides from hipcc is handled here:
 // the fragment reads are ordinary LDS loads (hipcc waits on lgkmcnt before the statement that reads them), each
 // accumulator is re-read 63 MFMAs after it was written, and the epilogue pads the MFMA -> accvgpr_read hazard itself.
+//
+// Operation kinds (one kernel body; the tile is 128 BYTES of k per row either way, and both MFMA shapes take 16
+// consecutive bytes of k per lane: A[row l & 15][bytes 16 (l >> 4) ..] -- 8 bf16 / fp16 or 16 int8):
+//   HG_BF16, HG_FP16   v_mfma_f32_16x16x32_{bf16,f16}, fp32 accumulators, one RNE rounding to T at the end
+//   HG_I8_DEQ          v_mfma_i32_16x16x64_i8, exact int32, the fused mm_dequant epilogue to fp16
+//                      (igemmlt + dequant_mm_int32_fp16, ref:sycl/sycl_code/kernel_quant.cpp:3969 order)
+//   HG_I8_I32          the same product stored as int32 (igemmlt's row-major int32 C)
+enum HgOp { HG_BF16 = 0, HG_FP16 = 1, HG_I8_DEQ = 2, HG_I8_I32 = 3 };
 typedef unsigned hg_u32x4_t __attribute__((ext_vector_type(4)));
-template <typename T> struct HgFrag;
-template <> struct HgFrag<bf16_t> {
-  typedef hg_u32x4_t type;
-  __device__ static __forceinline__ f32x4_t mma(const type& a, const type& b, f32x4_t c) {
+typedef int hg_i32x4_t __attribute__((ext_vector_type(4)));
+template <int OP> struct HgOpT;
+template <> struct HgOpT<HG_BF16> {
+  typedef f32x4_t acc_t;
+  static constexpr int ELEM = 2;
+  __device__ static __forceinline__ acc_t mma(const hg_u32x4_t& a, const hg_u32x4_t& b, acc_t c) {
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
     return c;
   }
-  __device__ static __forceinline__ f32x4_t mma0(const type& a, const type& b) {
-    f32x4_t c;
+  __device__ static __forceinline__ acc_t mma0(const hg_u32x4_t& a, const hg_u32x4_t& b) {
+    acc_t c;
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
     return c;
   }
 };
-template <> struct HgFrag<fp16_t> {
-  typedef hg_u32x4_t type;
-  __device__ static __forceinline__ f32x4_t mma(const type& a, const type& b, f32x4_t c) {
+template <> struct HgOpT<HG_FP16> {
+  typedef f32x4_t acc_t;
+  static constexpr int ELEM = 2;
+  __device__ static __forceinline__ acc_t mma(const hg_u32x4_t& a, const hg_u32x4_t& b, acc_t c) {
     asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
     return c;
   }
-  __device__ static __forceinline__ f32x4_t mma0(const type& a, const type& b) {
-    f32x4_t c;
+  __device__ static __forceinline__ acc_t mma0(const hg_u32x4_t& a, const hg_u32x4_t& b) {
+    acc_t c;
     asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
     return c;
   }
 };
+struct HgOpI8 {
+  typedef hg_i32x4_t acc_t;
+  static constexpr int ELEM = 1;
+  __device__ static __forceinline__ acc_t mma(const hg_u32x4_t& a, const hg_u32x4_t& b, acc_t c) {
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+    return c;
+  }
+  __device__ static __forceinline__ acc_t mma0(const hg_u32x4_t& a, const hg_u32x4_t& b) {
+    acc_t c;
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+    return c;
+  }
+};
+template <> struct HgOpT<HG_I8_DEQ> : HgOpI8 {};
+template <> struct HgOpT<HG_I8_I32> : HgOpI8 {};
+
+// The same without saving / restoring M0: valid only in a kernel whose code uses M0 for nothing else (k_hgemm: no
+// LDS-DMA builtin, no s_sendmsg / movrel / LDS-parameter access -- `grep m0` of its .s shows only these statements).
+// The s_nop 0 is the M0-write -> LDS-DMA wait state.
+__device__ __forceinline__ void glds16_sv_m0(const void* sbase, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
 
 __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r >> 1) & 7)) << 4); }
 
 // V: schedule variant bits (A/B arms of tools/hgemm_lab.hip; HG_V is the launched one):
 //   1 = step-1 fragment reads all after half 1's MFMAs, 2 = no sched_barrier fences in half 2,
 //   4 = next-step fragments read in MFMA-need order, 8 = DMA spread (8 pieces before the wait, 8 after, one per
-//   4 MFMAs) -- 1.6 PFLOP/s vs 1.44 for 0 at 4096 x 4096 x 11008 (profiles/lab/r03_hgemm_variants.txt)
-constexpr int HG_V = 8;
-template <typename T, int V = 0>
+//   4 MFMAs; 1.6 PFLOP/s vs 1.44 for 0 at 4096 x 4096 x 11008, profiles/lab/r03_hgemm_variants.txt), 16 = LDS-DMA
+//   without the M0 save / restore (another 2-3 %, profiles/lab/r03_hgemm_dma_variants.txt), 32 = 12 pieces before
+//   the wait (no gain).  Launched: 8 + 16.
+constexpr int HG_V = 24;
+// lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
+template <int OP, int V = 0>
 __global__ void __launch_bounds__(HG_THREADS, 1)
-k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __restrict__ B, long long ldb,
-        T* __restrict__ C, long long ldc) {
+k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const void* __restrict__ Bv, long long ldb,
+        void* __restrict__ Cv, long long ldc, const float* __restrict__ rowStats, const float* __restrict__ colStats,
+        const fp16_t* __restrict__ bias) {
+  using Op = HgOpT<OP>;
+  using acc_t = typename Op::acc_t;
+  constexpr int E = Op::ELEM;
+  const uint8_t* A = reinterpret_cast<const uint8_t*>(Av);
+  const uint8_t* B = reinterpret_cast<const uint8_t*>(Bv);
   __shared__ __attribute__((aligned(16))) uint8_t smem[HG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -115,7 +162,7 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
   // (32-bit arithmetic: the host keeps every offset below 4 GiB; 64-bit products made hipcc park each offset in a
   // 4-register tuple)
   uint32_t aoff[8], boff[8];
-  const uint32_t lda2 = (uint32_t)lda * 2u, ldb2 = (uint32_t)ldb * 2u;
+  const uint32_t lda2 = (uint32_t)lda * E, ldb2 = (uint32_t)ldb * E;   // row strides in bytes
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = 8 * (8 * wave + i) + (lane >> 3);
@@ -125,10 +172,12 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
   }
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem) + wave * 8192;
   auto dma_a = [&](int kt, int st, int i) {
-    glds16_sv(A + (long long)kt * HG_BK, aoff[i], lds0 + st * HG_STAGE + i * 1024);
+    if constexpr ((V & 16) != 0) glds16_sv_m0(A + (long long)kt * 128, aoff[i], lds0 + st * HG_STAGE + i * 1024);
+    else glds16_sv(A + (long long)kt * 128, aoff[i], lds0 + st * HG_STAGE + i * 1024);
   };
   auto dma_b = [&](int kt, int st, int i) {
-    glds16_sv(B + (long long)kt * HG_BK, boff[i], lds0 + st * HG_STAGE + HG_TILE + i * 1024);
+    if constexpr ((V & 16) != 0) glds16_sv_m0(B + (long long)kt * 128, boff[i], lds0 + st * HG_STAGE + HG_TILE + i * 1024);
+    else glds16_sv(B + (long long)kt * 128, boff[i], lds0 + st * HG_STAGE + HG_TILE + i * 1024);
   };
 
   // ---- fragments: MFMA A operand = B rows (n), MFMA B operand = A rows (m), so D[n][m] and a lane's 4 results
@@ -139,14 +188,14 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
   const int xo0 = (128 * wm + fr) * 128 + ((fg ^ key) << 4), xo1 = (128 * wm + fr) * 128 + (((4 + fg) ^ key) << 4);
   const int wo0 = HG_TILE + (128 * wn + fr) * 128 + ((fg ^ key) << 4);
   const int wo1 = HG_TILE + (128 * wn + fr) * 128 + (((4 + fg) ^ key) << 4);
-  using frag_t = typename HgFrag<T>::type;
+  using frag_t = hg_u32x4_t;
   auto rd = [&](int st, int off, int f) -> frag_t {
     return *reinterpret_cast<const frag_t*>(smem + st * HG_STAGE + off + f * 2048);
   };
 
-  f32x4_t acc[8][8];
+  acc_t acc[8][8];
   frag_t w0[8], x0[8], w1[8], x1[8];
-  const int nk = K / HG_BK;
+  const int nk = K * E / 128;                   // k-tiles of 128 bytes
 
   // half 1 of k-tile t (stage st): the 64 MFMAs of k32 step 0, step 1's fragments of the stage read underneath (one
   // read per 4 MFMAs); then this wave's reads are retired and the barrier says every wave is done with the stage.
@@ -156,8 +205,8 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
     for (int j = 0; j < 8; ++j) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        if constexpr (decltype(first)::value) acc[j][i] = HgFrag<T>::mma0(w0[j], x0[i]);
-        else acc[j][i] = HgFrag<T>::mma(w0[j], x0[i], acc[j][i]);
+        if constexpr (decltype(first)::value) acc[j][i] = Op::mma0(w0[j], x0[i]);
+        else acc[j][i] = Op::mma(w0[j], x0[i], acc[j][i]);
         if (!(V & 1) && (i & 3) == 3) {
           const int q = 2 * j + (i >> 2);               // 0..15
           if (q < 8) w1[q] = rd(st, wo1, q);
@@ -180,7 +229,9 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
   // fragments read under the last 32.
   auto half2 = [&](auto last, int t, int st) {
     constexpr bool L = decltype(last)::value;
-    constexpr bool SPREAD = (V & 8) != 0;    // 8 DMA pieces before the wait, 8 after (one per 4 MFMAs throughout)
+    // PRE of the 16 DMA pieces go in before the wait for tile t+1, spread over the first 32 MFMAs; the rest after it,
+    // spread over the last 32 (V & 8: 8 / 8; V & 32: 12 / 4; neither: 16 / 0, one per 2 MFMAs)
+    constexpr int PRE = (V & 32) ? 12 : (V & 8) ? 8 : 16;
     const int kn = min(t + 2, nk - 1);
     auto dma = [&](int q) {
       if (q < 8) dma_a(kn, st, q);
@@ -197,24 +248,29 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
         else x0[q - 8] = rd(st ^ 1, xo0, q - 8);
       }
     };
+    // DMA piece issued after MFMA `mi` (0..31) of a part holding `cnt` pieces: pieces land on MFMAs
+    // (q + 1) * 32 / cnt - 1, q = 0 .. cnt - 1 (evenly spread, the last one on the part's last MFMA)
+    auto piece_at = [](int mi, int cnt) -> int {
+      for (int q = 0; q < cnt; ++q)
+        if (((q + 1) * 32) / cnt - 1 == mi) return q;
+      return -1;
+    };
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        acc[j][i] = HgFrag<T>::mma(w1[j], x1[i], acc[j][i]);
+        acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
         if constexpr (!L) {
-          if (SPREAD) {
-            if ((i & 3) == 3) dma(2 * j + (i >> 2));            // pieces 0..7
-          } else if ((i & 1) == 1) {
-            dma(4 * j + (i >> 1));                              // pieces 0..15
-          }
+          const int q = piece_at(8 * j + i, PRE);
+          if (q >= 0) dma(q);
         }
       }
       if (!(V & 2)) __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (!L) {
-      if (SPREAD) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");    // tile t+1 landed (this wave's pieces)
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      if constexpr (PRE == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // tile t+1 landed (this wave)
+      else if constexpr (PRE == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       __builtin_amdgcn_s_barrier();                                    // ... every wave's pieces
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -222,10 +278,11 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
     for (int j = 4; j < 8; ++j) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        acc[j][i] = HgFrag<T>::mma(w1[j], x1[i], acc[j][i]);
+        acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
         if constexpr (!L) {
           if ((i & 1) == 1) rdn(4 * (j - 4) + (i >> 1));       // fragments 0..15
-          if (SPREAD && (i & 3) == 0) dma(8 + 2 * (j - 4) + (i >> 2));   // pieces 8..15
+          const int q = piece_at(8 * (j - 4) + i, 16 - PRE);
+          if (q >= 0) dma(PRE + q);
         }
       }
       if (!(V & 2)) __builtin_amdgcn_sched_barrier(0);
@@ -257,63 +314,129 @@ k_hgemm(int M, int N, int K, const T* __restrict__ A, long long lda, const T* __
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 
-  // ---- epilogue: acc[j][i][r] = C[m0 + 128 wm + 16 i + fr][n0 + 128 wn + 16 j + 4 fg + r]; 8-B stores.
-  // Full tiles (the common case) store unconditionally; edge tiles check every row / column.
+  // ---- epilogue: acc[j][i][r] = C[m0 + 128 wm + 16 i + fr][n0 + 128 wn + 16 j + 4 fg + r] -- four consecutive
+  // columns of one row per accumulator: one 8-B store (16-bit outputs) or 16-B store (int32).  Full tiles (the common
+  // case) store unconditionally; edge tiles check every row / column.
   const int mb = m0 + 128 * wm + fr, nb = n0 + 128 * wn + 4 * fg;
-  const bool full = (m0 + HG_BM <= M) && (n0 + HG_BN <= N) && ((ldc & 3) == 0) && (((uintptr_t)C & 7) == 0);
-  if (full) {
+  constexpr int OUT = (OP == HG_I8_I32) ? 4 : 2;
+  const bool full = (m0 + HG_BM <= M) && (n0 + HG_BN <= N) && (((ldc * OUT) & 15) == 0) &&
+                    (((uintptr_t)Cv & 15) == 0);
+  auto value = [&](int j, int i, int r, int n, float rs) -> float {   // HG_I8_DEQ: mm_dequant of one element
+    return (float)Io<fp16_t>::to_f32(mm_dequant_value(acc[j][i][r], rs, colStats[n], bias ? (float)bias[n] : 0.0f));
+  };
+  if (full && OUT == 2) {
+    // 16-bit outputs of a full tile: staged through LDS so every global store writes whole 256-B row segments
+    // (direct 8-B fragment stores put 16 rows x 32 B in one instruction: +4 us of epilogue per launch at 4096^2)
+    __syncthreads();                                   // every wave is past its last stage read
+    uint8_t* ep = smem + wave * (128 * HG_EPI_PITCH);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      T* crow = C + (long long)(mb + 16 * i) * ldc + nb;
+      float rs = 0.f;
+      if constexpr (OP == HG_I8_DEQ) rs = rowStats[mb + 16 * i];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         uint2 v;
-        v.x = cvt_pk<T>(acc[j][i][0], acc[j][i][1]);
-        v.y = cvt_pk<T>(acc[j][i][2], acc[j][i][3]);
-        *reinterpret_cast<uint2*>(crow + 16 * j) = v;
+        if constexpr (OP == HG_BF16 || OP == HG_FP16) {
+          using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
+          v.x = cvt_pk<T>(acc[j][i][0], acc[j][i][1]);
+          v.y = cvt_pk<T>(acc[j][i][2], acc[j][i][3]);
+        } else if constexpr (OP == HG_I8_DEQ) {
+          const int n = nb + 16 * j;
+          uint16_t h[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            h[r] = __builtin_bit_cast(uint16_t, mm_dequant_value(acc[j][i][r], rs, colStats[n + r],
+                                                                 bias ? (float)bias[n + r] : 0.0f));
+          v = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+        }
+        *reinterpret_cast<uint2*>(ep + (16 * i + fr) * HG_EPI_PITCH + 2 * (16 * j + 4 * fg)) = v;
         __builtin_amdgcn_sched_barrier(0);   // one accumulator at a time: no VGPR burst that displaces AGPRs
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): the wave reads back only its own region
+    uint8_t* cbase = reinterpret_cast<uint8_t*>(Cv) + ((long long)(m0 + 128 * wm) * ldc + n0 + 128 * wn) * 2;
+#pragma unroll 8
+    for (int it = 0; it < 32; ++it) {
+      const int row = 4 * it + (lane >> 4), c16 = lane & 15;
+      const uint4 v = *reinterpret_cast<const uint4*>(ep + row * HG_EPI_PITCH + 16 * c16);
+      *reinterpret_cast<uint4*>(cbase + (long long)row * ldc * 2 + 16 * c16) = v;
+    }
+  } else if (full) {
+    if constexpr (OP == HG_I8_I32) {                   // int32: one 16-B store per accumulator already
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const long long m = mb + 16 * i;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = nb + 16 * j;
+          *reinterpret_cast<hg_i32x4_t*>(reinterpret_cast<int32_t*>(Cv) + m * ldc + n) = acc[j][i];
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = mb + 16 * i;
-      T* crow = C + (long long)min(m, M - 1) * ldc;
+      const long long mc = min(m, M - 1);
+      float rs = 0.f;
+      if constexpr (OP == HG_I8_DEQ) rs = rowStats[mc];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = nb + 16 * j + r;
-          if (m < M && n < N) crow[n] = Io<T>::from_f32(acc[j][i][r]);
+          if (m < M && n < N) {
+            if constexpr (OP == HG_BF16) reinterpret_cast<bf16_t*>(Cv)[mc * ldc + n] = Io<bf16_t>::from_f32(acc[j][i][r]);
+            else if constexpr (OP == HG_FP16) reinterpret_cast<fp16_t*>(Cv)[mc * ldc + n] = Io<fp16_t>::from_f32(acc[j][i][r]);
+            else if constexpr (OP == HG_I8_DEQ)
+              reinterpret_cast<fp16_t*>(Cv)[mc * ldc + n] =
+                  mm_dequant_value(acc[j][i][r], rs, colStats[n], bias ? (float)bias[n] : 0.0f);
+            else reinterpret_cast<int32_t*>(Cv)[mc * ldc + n] = acc[j][i][r];
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
     }
   }
+  (void)value;
 }
 
-// Host rule: K % 64 == 0, 16-B aligned rows (lda, ldb % 8 == 0, 16-B aligned bases), and every lane offset
-// (row * ld * 2 bytes) below 4 GiB.
-bool hgemm_fits(int m, int n, int k, long long lda, long long ldb, const void* A, const void* B) {
-  if (m <= 0 || n <= 0 || k <= 0 || (k % HG_BK) != 0) return false;
-  if ((lda & 7) || (ldb & 7) || lda < k || ldb < k) return false;
+// Host rule: k bytes (k * element size) % 128 == 0, 16-B aligned rows and bases, and every lane offset
+// (row * ld * element size bytes) below 4 GiB.
+bool hgemm_fits(int m, int n, int k, long long lda, long long ldb, const void* A, const void* B, int elem) {
+  if (m <= 0 || n <= 0 || k <= 0 || ((long long)k * elem) % 128 != 0) return false;
+  if (((lda * elem) & 15) || ((ldb * elem) & 15) || lda < k || ldb < k) return false;
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return false;
-  if ((long long)(m - 1) * lda * 2 + 2LL * k > 0xFFFFFFFFLL) return false;
-  if ((long long)(n - 1) * ldb * 2 + 2LL * k > 0xFFFFFFFFLL) return false;
+  if ((long long)(m - 1) * lda * elem + (long long)k * elem > 0xFFFFFFFFLL) return false;
+  if ((long long)(n - 1) * ldb * elem + (long long)k * elem > 0xFFFFFFFFLL) return false;
   return true;
 }
 
-template <typename T>
-int hgemm_tn(int m, int n, int k, const T* A, long long lda, const T* B, long long ldb, T* C, long long ldc) {
-  if (!hgemm_fits(m, n, k, lda, ldb, A, B) || ldc < n) return 1;
-  const long long tiles = (long long)((m + HG_BM - 1) / HG_BM) * ((n + HG_BN - 1) / HG_BN);
-  hipLaunchKernelGGL((k_hgemm<T, HG_V>), dim3((unsigned)tiles), dim3(HG_THREADS), 0, current_stream(), m, n, k, A, lda, B,
-                     ldb, C, ldc);
+long long hgemm_tiles(int m, int n) { return (long long)((m + HG_BM - 1) / HG_BM) * ((n + HG_BN - 1) / HG_BN); }
+
+template <int OP>
+int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* B, long long ldb, void* C, long long ldc,
+                 const float* rowStats = nullptr, const float* colStats = nullptr, const fp16_t* bias = nullptr) {
+  if (!hgemm_fits(m, n, k, lda, ldb, A, B, HgOpT<OP>::ELEM) || ldc < n) return 1;
+  hipLaunchKernelGGL((k_hgemm<OP, HG_V>), dim3((unsigned)hgemm_tiles(m, n)), dim3(HG_THREADS), 0, current_stream(), m,
+                     n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error((int)e, "k_hgemm launch");
     return 2;
   }
   return 0;
+}
+
+// int8 row-major igemmlt on the 4-wave kernel (int8.hip's launch_igemm takes it for large tile grids): 0 = launched,
+// 1 = not covered (the caller's kernels run), 2 = launch error
+int igemm_4wave(int m, int n, int k, const int8_t* A, long long lda, const int8_t* B, long long ldb, void* C,
+                long long ldc, bool dequant, const float* rowStats, const float* colStats, const fp16_t* bias) {
+  // HG_I8_I32 is not launched: its epilogue needs spill registers, and a spill the allocator places between the last
+  // (inline-asm, hazard-invisible) MFMAs and the wait-state pad reads accumulators before they are written (wrong
+  // int32 at ragged shapes, caught by tests/test_hgemm_gpu.py).  The launched kinds compile spill-free.
+  if (!dequant) return 1;
+  return hgemm_launch<HG_I8_DEQ>(m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias);
 }
 
 }  // namespace bnb
@@ -325,10 +448,10 @@ extern "C" {
 // ref:python_src_quants/autograd/_functions.py:507).  Returns 0 = launched, 1 = shape / alignment not supported
 // (k % 64, 16-B aligned rows; nothing launched), 2 = launch error (cget_last_error*).
 int chgemm_tn_bf16(int m, int n, int k, const bf16_t* A, int lda, const bf16_t* W, int ldw, bf16_t* C, int ldc) {
-  return bnb::hgemm_tn<bf16_t>(m, n, k, A, lda, W, ldw, C, ldc);
+  return bnb::hgemm_launch<bnb::HG_BF16>(m, n, k, A, lda, W, ldw, C, ldc);
 }
 int chgemm_tn_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* W, int ldw, fp16_t* C, int ldc) {
-  return bnb::hgemm_tn<fp16_t>(m, n, k, A, lda, W, ldw, C, ldc);
+  return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc);
 }
 
 }  // extern "C"

@@ -610,13 +610,24 @@ k_igemm(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restr
   }
 }
 
-static int g_igemm_tile = 0;   // 0 = auto, 128 = force the 128x128 register-staged kernel (tests / A-B)
+static int g_igemm_tile = 0;   // 0 = auto, 128 = force the 128x128 register-staged kernel, 4 = the 4-wave
+                               // hgemm.hip kernel for row-major operands (tests / A-B)
 
 template <int AF, int BF, int EPI>
 static int launch_igemm(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale, long long lda,
                         long long ldb, long long ldc, const float* rowStats = nullptr, const float* colStats = nullptr,
                         const fp16_t* bias = nullptr, int32_t* ws = nullptr, long long ws_bytes = 0) {
   if (m <= 0 || n <= 0 || k <= 0) return 0;
+  // row-major operands on the 4-wave kernel (hgemm.hip HG_I8_*, one wave per SIMD, 128 x 128 per wave) only when
+  // forced (cigemm_set_tile(4)): bit-identical, but 163 vs 142 us at 4096 x 4096 x 11008 and 82 vs 60 us at 4096^3
+  // against igemm_256's 8 waves (tools/int8_4wave_ab.py, profiles/lab/r03_int8_4wave_ab.txt) -- the int8 MFMA
+  // stream wants the second wave per SIMD that the bf16 one does not
+  if constexpr (AF == ROW && BF == ROW && (EPI == EPI_F16_ROW_DEQUANT || EPI == EPI_I32_ROW)) {
+    if (g_igemm_tile == 4 && hgemm_tiles(m, n) >= 1) {
+      const int rc = igemm_4wave(m, n, k, A, lda, B, ldb, C, ldc, EPI == EPI_F16_ROW_DEQUANT, rowStats, colStats, bias);
+      if (rc != 1) return rc == 0 ? 0 : 1;
+    }
+  }
   // large problems: 256x256 LDS-DMA kernel (igemm_256.hip; split-K over ws for small tile grids); small /
   // col_turing / ragged-k: 128x128 here
   if (g_igemm_tile != 128 &&

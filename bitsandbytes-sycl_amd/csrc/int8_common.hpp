@@ -51,6 +51,10 @@ bool launch_igemm_256(int m, int n, int k, const int8_t* A, const int8_t* B, voi
                       long long lda, long long ldb, long long ldc, const float* rowStats, const float* colStats,
                       const fp16_t* bias, int32_t* ws = nullptr, long long ws_bytes = 0);
 int igemm_splitk_factor(int m, int n, int k);
+// row-major int8 product on the 4-wave 256 x 256 kernel (hgemm.hip): 0 = launched, 1 = not covered, 2 = launch error
+int igemm_4wave(int m, int n, int k, const int8_t* A, long long lda, const int8_t* B, long long ldb, void* C,
+                long long ldc, bool dequant, const float* rowStats, const float* colStats, const fp16_t* bias);
+long long hgemm_tiles(int m, int n);
 long long igemm_workspace_bytes(int m, int n, int k);
 
 }  // namespace bnb

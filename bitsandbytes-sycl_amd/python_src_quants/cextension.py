@@ -41,7 +41,7 @@ class BNBNativeLibrary:
                      "cigemmlt_ampere_32", "cigemmlt_ampere_8", "cigemmlt_ampere_8_rowscale",
                      "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cigemmlt_row_dequant_ws_fp16",
                      "cigemm_row_i32_ws", "cgemm_tn_bf16", "cgemm_tn_fp16", "cgemm_tn_set_search", "cgemm_tn_plan",
-                     "chgemm_tn_bf16", "chgemm_tn_fp16",
+                     "chgemm_tn_bf16", "chgemm_tn_fp16", "cprobe_mfma", "cprobe_hbm_read",
                      "cget_last_error", "cget_abi_version",
                      "cgemm_4bit_inference_naive_nested_fp16", "cgemm_4bit_inference_naive_nested_bf16",
                      "cdequantize_blockwise_nested_fp16_fp4", "cdequantize_blockwise_nested_fp16_nf4",

@@ -193,6 +193,12 @@ class ColumnShardedLinear4bit(torch.nn.Module):
             return F.gemv_4bit(x2, self.qweight.t(), state=self.quant_state)
         return F.gemm_4bit(x2, self.qweight, self.quant_state)
 
+    def decode_step(self, dtype=torch.bfloat16) -> ShardedDecode:
+        """A static-buffer M = 1 step (this shard's GEMV + one all-gather) for graph capture: ShardedDecode."""
+        fn = lambda x, y: F.gemv_4bit(x, self.qweight.t(), out=y, state=self.quant_state)  # noqa: E731
+        return ShardedDecode(fn, self.in_features, self.end - self.start, self.world, self.group, dtype,
+                             self.qweight.device)
+
     def forward(self, x: torch.Tensor, assemble: bool = True, chunks: int = 1) -> torch.Tensor:
         """chunks > 1 overlaps the all-gather of each token-row chunk with the next chunk's GEMM
         (result layout [chunks, world, M/chunks, n] when assemble=False)."""
@@ -211,6 +217,66 @@ class ColumnShardedLinear4bit(torch.nn.Module):
             return sharded_forward_overlapped(x2, mm, self.world, self.group, chunks, rows_out=rows)
         g = gather_columns(self.forward_local(x), self.world, self.group)
         return gathered_to_rows(g) if assemble else g
+
+
+class ShardedDecode:
+    """The M = 1 (decode) forward of a column-sharded layer on static buffers, so one decode step -- this rank's GEMV
+    into `y` [1, n], ONE all-gather of the KB-sized shard outputs into `gathered` [world, 1, n] and the [1, world*n]
+    row assembled in `rows` -- can be captured in a HIP graph and replayed (at M = 1 the all-gather is
+    latency-bound; replaying the captured step removes the host launch cost of the GEMV, the collective and the copy,
+    which is most of a decode step's time at these sizes).  `local_fn(x, y)` writes this rank's [1, n] slice of x
+    [1, K] into y (ColumnShardedLinear4bit.decode_step passes the GEMV); the input goes through `set_input`."""
+
+    def __init__(self, local_fn: Callable, in_features: int, n_local: int, world: int, group=None,
+                 dtype=torch.bfloat16, device=None):
+        self.local_fn, self.world, self.group = local_fn, world, group
+        self.x = torch.zeros(1, in_features, dtype=dtype, device=device)
+        self.y = torch.empty(1, n_local, dtype=dtype, device=device)
+        self.gathered = torch.empty(world, 1, n_local, dtype=dtype, device=device)
+        self.rows = torch.empty(1, world * n_local, dtype=dtype, device=device)
+        self.graph = None
+
+    def set_input(self, x: torch.Tensor):
+        self.x.copy_(x.reshape(self.x.shape))
+
+    def step(self) -> torch.Tensor:
+        """One eager decode step on the static buffers; returns `rows`."""
+        self.local_fn(self.x, self.y)
+        gather_columns(self.y, self.world, self.group, out=self.gathered)
+        if self.world == 1:
+            self.gathered[0].copy_(self.y)
+        self.rows.view(1, self.world, -1).copy_(self.gathered.permute(1, 0, 2))
+        return self.rows
+
+    def capture(self, warmup: int = 2) -> bool:
+        """Capture step() into a HIP graph (side-stream warm-up first, as torch.cuda.graph requires).  Returns False
+        (and leaves eager mode) when the backend cannot be captured (gloo, or a collective capture refused)."""
+        if not self.x.is_cuda or (self.world > 1 and dist.get_backend(self.group) == "gloo"):
+            return False
+        s = torch.cuda.Stream(device=self.x.device)
+        s.wait_stream(torch.cuda.current_stream(self.x.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step()
+        torch.cuda.current_stream(self.x.device).wait_stream(s)
+        torch.cuda.synchronize(self.x.device)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self.step()
+        except Exception:  # noqa: BLE001 - capture refused: stay eager
+            torch.cuda.synchronize(self.x.device)
+            return False
+        self.graph = g
+        return True
+
+    def __call__(self, x: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if x is not None:
+            self.set_input(x)
+        if self.graph is not None:
+            self.graph.replay()
+            return self.rows
+        return self.step()
 
 
 class ColumnShardedLinear8bitLt(torch.nn.Module):

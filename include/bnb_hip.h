@@ -211,9 +211,16 @@ int cgemm_tn_plan(int m, int n, int k, int dtype, int lda, int ldw, int ldc);
  * 16-B aligned; nothing launched), 2 = launch error (cget_last_error*). */
 int chgemm_tn_bf16(int m, int n, int k, const bnb_bf16* A, int lda, const bnb_bf16* W, int ldw, bnb_bf16* C, int ldc);
 int chgemm_tn_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp16* W, int ldw, bnb_fp16* C, int ldc);
+/* [additive, measurement] measured ceilings for the bench's roofline (probe.hip): the dense MFMA rate on random operands
+ * in registers (kind 0 = bf16 v_mfma_f32_16x16x32_bf16, 1 = int8 v_mfma_i32_16x16x64_i8; one wave per SIMD, 8 x iters
+ * MFMAs per wave; sink >= blocks * 256 floats) and the HBM streaming read rate (bytes % 16 == 0; sink >= blocks
+ * dwords).  Return 0 = launched, 1 = bad kind, 2 = launch error. */
+int cprobe_mfma(int kind, int blocks, int iters, unsigned seed, float* sink);
+int cprobe_hbm_read(const void* p, long long bytes, int blocks, unsigned* sink);
 /* [additive, testing] int8 split-K factor: -1 = auto, 1 = never, >= 2 = force where it applies */
 void cigemm_set_splitk(int ks);
-/* [additive, testing] force the int8 GEMM tile kernel: 0 = auto (256x256 when it applies), 128 = 128x128 */
+/* [additive, testing] force the int8 GEMM tile kernel: 0 = auto (256x256 when it applies), 128 = 128x128, 4 = the
+ * 4-wave 256x256 kernel of hgemm.hip for row-major operands (A/B only: slower than the default for int8) */
 void cigemm_set_tile(int tile);
 
 /* ---- int32 -> fp16 dequant: ref:sycl/pythonInterface.cpp:333 ----

@@ -283,6 +283,33 @@ def gemv_4bit(x: np.ndarray, packed: np.ndarray, absmax: np.ndarray, N: int, K: 
     return W @ np.asarray(x, dtype=np.float64).reshape(K)
 
 
+def round_to(x: np.ndarray, dtype: str) -> np.ndarray:
+    """fp32 -> T -> fp32 with one round-to-nearest-even (T = bf16 or fp16)."""
+    x = np.asarray(x, dtype=F32)
+    if dtype == "bf16":
+        return bf16_bits_to_f32(f32_to_bf16_bits(x))
+    if dtype == "fp16":
+        return x.astype(np.float16).astype(F32)
+    return x
+
+
+def gemv_4bit_ref_faithful(x: np.ndarray, packed: np.ndarray, absmax: np.ndarray, N: int, K: int,
+                           blocksize: int, table: np.ndarray, dtype: str) -> np.ndarray:
+    """The reference GEMV WITH its T-precision arithmetic: kgemm_4bit_inference_naive
+    (ref:sycl/sycl_code/kernel_gemm.cpp:1291-1294, 1305, 1336-1343, DPCT_COMPATIBILITY_TEMP >= 800 branch) holds the
+    16-entry code table and the block absmax in T (`quant_map[i] = T(datatype[i])`, `T local_absmax`), forms each
+    weight as a T product (`local_B = quant_map[q] * local_absmax`, rounded to T) and each activation x weight product
+    in T (`(float)(local_A[k] * local_B[k])`), accumulating those in fp32.  Here: the same roundings, the sum of the
+    T-rounded products in fp64 (the kernel's per-lane fp32 order differs from any fixed order by far less than the
+    T roundings).  x is given as its T values."""
+    q = unpack_4bit(packed, N * K).reshape(N, K)
+    tab = round_to(np.asarray(table, dtype=F32), dtype)
+    am = round_to(np.repeat(np.asarray(absmax, dtype=F32), blocksize)[: N * K].reshape(N, K), dtype)
+    w = round_to(tab[q] * am, dtype)
+    prod = round_to(w * round_to(np.asarray(x, dtype=F32).reshape(1, K), dtype), dtype)
+    return prod.astype(np.float64).sum(axis=1)
+
+
 def gemm_4bit_dequant_ref(X: np.ndarray, packed: np.ndarray, absmax: np.ndarray, N: int, K: int,
                           blocksize: int, table: np.ndarray, weight_dtype: str = "bf16") -> np.ndarray:
     """Reference M>1 path (autograd/_functions.py:507): W = dequantize_4bit (one RNE cast to the

@@ -192,3 +192,28 @@ def test_matmullt(dev, dims, decomp, dtype, req_grad, transpose, has_fp16_weight
                 torch.testing.assert_close(gradB1, gradB2, atol=0.18, rtol=0.3)
             if req_grad[2]:
                 torch.testing.assert_close(gradBias1, gradBias2)
+
+
+def test_matmul_4bit_single_row_routing(dev):
+    """One activation row without gradient follows the reference's routing (ref:autograd/_functions.py:557-577):
+    gemv_4bit(A, B.t()) whatever orientation B is passed in -- so it computes A @ W^T from quant_state's shape.  With
+    the transposed view (Linear4bit's weight.t()) that is the requested product; with the untransposed storage the
+    reference computes the same A @ W^T (square W) or a width-mismatched GEMV, which this build rejects with a
+    ValueError instead of returning garbage."""
+    bnb = _bnb()
+    F = bnb.functional
+    torch.manual_seed(3)
+    for n_out, k_in in ((256, 128), (128, 128)):
+        W = torch.randn(n_out, k_in, device=dev, dtype=torch.bfloat16) * 0.05
+        q, st = F.quantize_4bit(W, quant_type="nf4")
+        Wd = F.dequantize_4bit(q, st).float()
+        a = torch.randn(1, k_in, device=dev, dtype=torch.bfloat16)
+        y = bnb.matmul_4bit(a, q.t(), st)
+        assert y.shape == (1, n_out)
+        assert torch.allclose(y.float(), a.float() @ Wd.t(), atol=2e-2, rtol=2e-2)
+        if n_out == k_in:
+            y2 = bnb.matmul_4bit(a, q, st)                 # reference routing: the same GEMV
+            assert torch.equal(y2, y)
+        else:
+            with pytest.raises(ValueError):
+                bnb.matmul_4bit(torch.randn(1, n_out, device=dev, dtype=torch.bfloat16), q, st)

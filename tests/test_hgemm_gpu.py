@@ -132,3 +132,30 @@ def test_gemm_4bit_hgemm_route_vs_oracle(dev, dtype, nested):
     got = Y.float().cpu().numpy().astype(np.float64)
     rms = np.sqrt(np.mean(exp ** 2))
     assert np.all(np.abs(got - exp) <= tol * rms + tol * np.abs(exp))
+
+
+@pytest.mark.parametrize("mnk", [(4096, 4096, 4096), (700, 900, 1024), (256, 512, 128)])
+def test_int8_on_the_4wave_kernel_is_bit_identical(dev, mnk):
+    """The same kernel body for int8 (HG_I8_DEQ, forced by cigemm_set_tile(4)): the fused mm_dequant bits equal the
+    default int8 kernels' (igemm_256 / the 128-tile kernel) -- both exact int32 sums then the same dequant.  The int32
+    product itself (igemm_rowmajor) stays on the default kernels under the knob; checked exact here."""
+    F = _F()
+    m, n, k = mnk
+    g = torch.Generator(device=dev).manual_seed(m + k)
+    A = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8, generator=g)
+    B = torch.randint(-127, 128, (n, k), device=dev, dtype=torch.int8, generator=g)
+    rs = torch.rand(m, device=dev, generator=g) * 2 + 0.5
+    cs = torch.rand(n, device=dev, generator=g) * 2 + 0.5
+    bias = torch.randn(n, device=dev, generator=g).half()
+    outs = {}
+    try:
+        for tile in (4, 0):
+            F.lib.cigemm_set_tile(tile)
+            outs[tile] = (F.igemmlt_dequant(A, B, rs, cs, bias=bias), F.igemm_rowmajor(A, B))
+    finally:
+        F.lib.cigemm_set_tile(0)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[4][1], outs[0][1])
+    assert torch.equal(outs[4][0], outs[0][0])
+    exact = (A.double() @ B.double().t())
+    assert torch.equal(outs[4][1].double(), exact)

@@ -1,0 +1,33 @@
+"""Build-time invariant of the kernels that issue MFMAs from inline asm (csrc/hgemm.hip, csrc/probe.hip): they must
+compile without register spills.  hipcc's hazard recognizer does not see an asm MFMA, so a spill the allocator
+placed between the last MFMAs and the hand-written wait-state pad would read accumulators before they are written
+(the HG_I8_I32 form did: wrong int32 at ragged shapes).  CPU-only: hipcc cross-compiles for gfx950 here."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "bitsandbytes-sycl_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.parametrize("src,kernel", [("hgemm.hip", "k_hgemm"), ("probe.hip", "k_probe_mfma")])
+def test_asm_mfma_kernels_compile_spill_free(tmp_path, src, kernel):
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-I", CSRC,
+                        "-c", os.path.join(CSRC, src), "-o", str(tmp_path / "k.o"),
+                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    names, spills = [], []
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            names.append(m.group(1))
+        m = re.search(r"VGPRs Spill: (\d+)", line)
+        if m and names and kernel in names[-1]:
+            spills.append((names[-1], int(m.group(1))))
+    assert spills, "no kernels found"
+    assert all(n == 0 for _, n in spills), spills

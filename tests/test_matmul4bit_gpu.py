@@ -88,6 +88,36 @@ def test_gemv_functional(dev, dtype, qt, shape):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+def test_gemv_c2_tolerance_covers_ref_faithful_variant(dev, dtype, nested, qt):
+    """Q8: the reference's GEMV holds the code table and absmax in T and rounds every weight and
+    every x * w product to T (ref:sycl/sycl_code/kernel_gemm.cpp:1291-1294, 1305, 1336-1343); this build computes
+    the weight in fp32 and accumulates fp32 dot products.  At config 2 (11008 x 4096) both the HIP output and the
+    ref-faithful restatement (oracle.ref.gemv_4bit_ref_faithful) sit within the stated tolerance of the fp64 oracle
+    (|d| <= tol * rms + tol * |ref|, tol 2e-2 bf16 / 1e-2 fp16), and within twice it of each other."""
+    F = _F()
+    N, K = 11008, 4096
+    torch.manual_seed(41 + nested)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type=qt, compress_statistics=nested)
+    del W
+    x = torch.randn(1, K, device=dev, dtype=dtype)
+    y = F.gemv_4bit(x, q.t(), state=st).float().cpu().numpy()[0]
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    xn, qn, code = x.float().cpu().numpy()[0], q.cpu().numpy(), st.code.cpu().numpy()
+    exp = ref.gemv_4bit(xn, qn, absmax, N, K, 64, code)
+    faithful = ref.gemv_4bit_ref_faithful(xn, qn, absmax, N, K, 64, code, "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    frac, err = _close(y, exp, tol, tol)
+    assert frac == 0.0, ("hip", err)
+    frac, err = _close(faithful, exp, tol, tol)
+    assert frac == 0.0, ("ref-faithful", err)
+    frac, err = _close(y, faithful, 2 * tol, 2 * tol)
+    assert frac == 0.0, ("hip vs ref-faithful", err)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(11008, 4096), (513, 6144), (4096, 11008), (64, 192)])
 def test_gemv_nested_fused_matches_two_step(dev, dtype, shape):
     """The in-kernel decode of compressed statistics is bit-identical to dequantize_blockwise(absmax) +

@@ -145,3 +145,24 @@ def test_cpu_path_semantics():
     assert q[1] == 0                   # -1 -> forced code[0]
     y = ref.dequantize_cpu(code2, q, absmax, 4)
     assert np.abs(y - A).max() < 0.02
+
+
+def test_gemv_tolerance_covers_ref_faithful_variant():
+    """Q8 on the CPU: the reference GEMV's T-precision arithmetic (oracle.ref.gemv_4bit_ref_faithful, table / absmax /
+    weights / products rounded to T, ref:sycl/sycl_code/kernel_gemm.cpp:1291-1294, 1336-1343) stays inside the stated
+    GEMV tolerance of the fp64 oracle (2e-2 bf16, 1e-2 fp16 of rms + |ref|), so the tolerance covers both the
+    reference's rounding and this build's fp32 weights.  The GPU test at config 2 is
+    test_matmul4bit_gpu.py::test_gemv_c2_tolerance_covers_ref_faithful_variant."""
+    rng = np.random.default_rng(8)
+    N, K = 1024, 4096
+    W = (rng.standard_normal((N, K)) * 0.02).astype(np.float32)
+    for qt in ("nf4", "fp4"):
+        am, q = ref.quantize_blockwise(W.reshape(-1), 64, qt)
+        table = ref.nf4_table() if qt == "nf4" else ref.fp4_table()
+        for dt, tol in (("bf16", 2e-2), ("fp16", 1e-2)):
+            x = ref.round_to(rng.standard_normal(K).astype(np.float32), dt)
+            exp = ref.gemv_4bit(x, q, am, N, K, 64, table)
+            got = ref.gemv_4bit_ref_faithful(x, q, am, N, K, 64, table, dt)
+            rms = np.sqrt(np.mean(exp ** 2))
+            assert np.all(np.abs(got - exp) <= tol * rms + tol * np.abs(exp)), (qt, dt)
+            assert not np.array_equal(got, exp)      # the variant does round differently

@@ -219,3 +219,50 @@ def test_int8_row_shard_gloo():
     ret = mgr.dict()
     mp.spawn(_worker_int8, args=(world, port, ret), nprocs=world, join=True)
     assert all(ret[r] for r in range(world))
+
+
+def _worker_decode(rank, world, port, ret):
+    """ShardedDecode (the M = 1 step the multi-GPU bench captures in a HIP graph) on CPU tensors over gloo: each rank's
+    GEMV is the oracle's gemv_4bit of its shard; the static-buffer step gathers and assembles the full decode row."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "bitsandbytes-sycl_amd")]
+    from oracle import ref
+    from python_src_quants.parallel import ShardedDecode
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, K, bs = 96, 128, 64
+        rng = np.random.default_rng(5)
+        W = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+        absmax, q = ref.quantize_blockwise(W.reshape(-1), bs, "nf4")
+        n = N // world
+        qs = q[rank * n * K // 2:(rank + 1) * n * K // 2]
+        am = absmax[rank * n * K // bs:(rank + 1) * n * K // bs]
+
+        def local(x, y):
+            y.copy_(torch.from_numpy(ref.gemv_4bit(x.numpy().reshape(-1), qs, am, n, K, bs,
+                                                   ref.nf4_table()).astype(np.float32)).view(1, n))
+        dec = ShardedDecode(local, K, n, world, dtype=torch.float32, device="cpu")
+        ok = dec.capture() is False                      # gloo / CPU: eager
+        for seed in (1, 2):
+            x = rng.standard_normal(K).astype(np.float32)
+            got = dec(torch.from_numpy(x).view(1, K)).numpy().reshape(-1)
+            exp = ref.gemv_4bit(x, q, absmax, N, K, bs, ref.nf4_table()).astype(np.float32)
+            ok &= bool(np.array_equal(got, exp))
+        ret[rank] = ok
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_decode_step_gloo():
+    """The M = 1 sharded forward on static buffers (ShardedDecode): per-rank GEMV + one all-gather assembles the
+    unsharded decode output exactly, repeatedly on the same buffers."""
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker_decode, args=(world, port, ret), nprocs=world, join=True)
+    assert all(ret[r] for r in range(world))

@@ -24,6 +24,7 @@ import csv, glob, sys
 rows = [r for p in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True) for r in csv.DictReader(open(p))
         if 'Cijk' in r['Name']]
 print(max(rows, key=lambda r: int(r['Calls']))['Name'] if rows else 'Cijk')" $OUT/trace) ;;
+  k_hgemm*) MATCH="k_hgemm" ;;
   *) MATCH="k_gemm_4bit_256" ;;
 esac
 python3 tools/pmc_traffic.py $OUT/fetch $OUT/write "$MATCH" $OUT/pmc_traffic.json 4096 4096 11008 "$LABEL" $OUT/mfma $OUT/trace || exit 4
