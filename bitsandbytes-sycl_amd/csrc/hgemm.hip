@@ -220,7 +220,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       for (int f = 0; f < 8; ++f) { w1[f] = rd(st, wo1, f); x1[f] = rd(st, xo1, f); }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);                   // lgkmcnt(0): this wave's reads of stage st are done
-    __builtin_amdgcn_s_barrier();                         // ... and every other wave's
+    if constexpr ((V & 256) == 0) __builtin_amdgcn_s_barrier();   // ... and every other wave's (V & 256: lab ablation)
     __builtin_amdgcn_sched_barrier(0);
   };
   // half 2 of k-tile t: the 64 MFMAs of step 1.  Unless LAST: tile t+2's DMA into stage st under the first 32 (one
@@ -268,10 +268,12 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       if (!(V & 2)) __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (!L) {
-      if constexpr (PRE == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // tile t+1 landed (this wave)
+      // (V & 64 / V & 128: lab ablations that drop the wait / the barrier -- wrong results, timing only)
+      if constexpr ((V & 64) != 0) {
+      } else if constexpr (PRE == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // tile t+1 landed (this wave)
       else if constexpr (PRE == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      __builtin_amdgcn_s_barrier();                                    // ... every wave's pieces
+      if constexpr ((V & 128) == 0) __builtin_amdgcn_s_barrier();      // ... every wave's pieces
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll

@@ -6,7 +6,7 @@ TAG=${1:-r01}
 OUT=gpurun_out
 mkdir -p $OUT
 if [ "$2" != "skip-tests" ]; then
-  timeout -k 10 600 python -m pytest tests -x -q -m gpu > $OUT/gpu_tests_$TAG.log 2>&1 || { echo "tests failed"; tail -30 $OUT/gpu_tests_$TAG.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests_$TAG.log 2>&1 || { echo "tests failed"; tail -30 $OUT/gpu_tests_$TAG.log; exit 1; }
   tail -2 $OUT/gpu_tests_$TAG.log
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke_$TAG.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke_$TAG.log; exit 2; }
   tail -1 $OUT/smoke_$TAG.log

@@ -99,19 +99,16 @@ int main(int argc, char** argv) {
     agree(name);
   };
   check(k_hgemm<HG_BF16, 24>, "hgemm v24");
-  check(k_hgemm<HG_BF16, 28>, "hgemm v28");
-  check(k_hgemm<HG_BF16, 26>, "hgemm v26");
-  check(k_hgemm<HG_BF16, 52>, "hgemm v52");
   const int R = 20;
   for (int r = 0; r < rounds; ++r) {
     const double t_lib = timeit(lib, R);
     double tv[4];
     tv[0] = timeit([&] { mine(k_hgemm<HG_BF16, 24>); }, R);
-    tv[1] = timeit([&] { mine(k_hgemm<HG_BF16, 28>); }, R);
-    tv[2] = timeit([&] { mine(k_hgemm<HG_BF16, 26>); }, R);
-    tv[3] = timeit([&] { mine(k_hgemm<HG_BF16, 52>); }, R);
+    tv[1] = timeit([&] { mine(k_hgemm<HG_BF16, 24 + 64>); }, R);
+    tv[2] = timeit([&] { mine(k_hgemm<HG_BF16, 24 + 128>); }, R);
+    tv[3] = timeit([&] { mine(k_hgemm<HG_BF16, 24 + 64 + 128 + 256>); }, R);
     printf("round %d  rocblas %7.1f us %6.0f TF |", r, t_lib, flop / t_lib / 1e6);
-    const int vs[4] = {24, 28, 26, 52};
+    const int vs[4] = {24, 24 + 64, 24 + 128, 24 + 448};
     for (int v = 0; v < 4; ++v) printf(" v%d %7.1f us %6.0f TF |", vs[v], tv[v], flop / tv[v] / 1e6);
     printf("\n");
     fflush(stdout);
