@@ -123,6 +123,14 @@ __device__ __forceinline__ void glds16_sv_m0(const void* sbase, uint32_t voff, u
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
 
+// Chained form: M0 already holds this piece's LDS address (set >= 1 instruction earlier); afterwards it is advanced by
+// `step` for the next piece, which must follow at least one other instruction later (the M0 -> LDS-DMA wait state).
+template <int STEP>
+__device__ __forceinline__ void glds16_chain(const void* sbase, uint32_t voff) {
+  asm volatile("global_load_lds_dwordx4 %0, %1\n\ts_add_u32 m0, m0, %2" : : "v"(voff), "s"(sbase), "i"(STEP) : "memory");
+}
+__device__ __forceinline__ void hg_set_m0(uint32_t lds) { asm volatile("s_mov_b32 m0, %0" : : "s"(lds) : "memory"); }
+
 __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r >> 1) & 7)) << 4); }
 
 // V: schedule variant bits (A/B arms of tools/hgemm_lab.hip; HG_V is the launched one):
@@ -130,8 +138,11 @@ __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r
 //   4 = next-step fragments read in MFMA-need order, 8 = DMA spread (8 pieces before the wait, 8 after, one per
 //   4 MFMAs; 1.6 PFLOP/s vs 1.44 for 0 at 4096 x 4096 x 11008, profiles/lab/r03_hgemm_variants.txt), 16 = LDS-DMA
 //   without the M0 save / restore (another 2-3 %, profiles/lab/r03_hgemm_dma_variants.txt), 32 = 12 pieces before
-//   the wait (no gain).  Launched: 8 + 16.
-constexpr int HG_V = 24;
+//   the wait (no gain), 4096 = M0 chained from piece to piece (one s_add per piece instead of s_add + s_mov + s_nop:
+//   another 2-3 %, profiles/lab/r03_hgemm_m0_chain.txt).  Lab-only ablations (wrong results, timing only): 64 = no
+//   vmcnt wait, 128 / 256 = no barrier B2 / B1, 512 = register-staged copies (slower: 256 vs 242 us), 1024 = no
+//   copies, 2048 = no fragment re-reads (profiles/lab/r03_hgemm_ablation.txt).  Launched: 8 + 16 + 4096.
+constexpr int HG_V = 8 + 16 + 4096;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
 template <int OP, int V = 0>
 __global__ void __launch_bounds__(HG_THREADS, 1)
@@ -197,17 +208,42 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   frag_t w0[8], x0[8], w1[8], x1[8];
   const int nk = K * E / 128;                   // k-tiles of 128 bytes
 
+  // V & 512 (lab): register-staged copies instead of LDS-DMA -- ordinary 16-B global loads into 16 staging registers
+  // (same swizzled source offsets), written to the same LDS slots one k-tile later by ds_write_b128.  The writes of
+  // tile t+1 finish before half 1's barrier, so that barrier alone orders them against the reads: one barrier per
+  // k-tile, no vmcnt bookkeeping of ours (hipcc counts the ordinary loads).
+  constexpr bool RS = (V & 512) != 0;
+  frag_t sg[RS ? 16 : 1];
+  auto rs_load = [&](int kt, int q) {
+    if constexpr (RS) {
+      const uint8_t* base = (q < 8 ? A : B) + (long long)kt * 128;
+      sg[q] = *reinterpret_cast<const frag_t*>(base + (q < 8 ? aoff[q] : boff[q - 8]));
+    }
+  };
+  auto rs_write = [&](int st, int q) {
+    if constexpr (RS)
+      *reinterpret_cast<frag_t*>(smem + st * HG_STAGE + (q < 8 ? 0 : HG_TILE) + wave * 8192 + (q & 7) * 1024 +
+                                 16 * lane) = sg[q];
+  };
+
   // half 1 of k-tile t (stage st): the 64 MFMAs of k32 step 0, step 1's fragments of the stage read underneath (one
   // read per 4 MFMAs); then this wave's reads are retired and the barrier says every wave is done with the stage.
   // FIRST: tile 0 starts the accumulators (SrcC = 0, so no zero-fill of the AGPRs is needed).
-  auto half1 = [&](auto first, int st) {
+  auto half1 = [&](auto first, int t) {
+    const int st = t & 1;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         if constexpr (decltype(first)::value) acc[j][i] = Op::mma0(w0[j], x0[i]);
         else acc[j][i] = Op::mma(w0[j], x0[i], acc[j][i]);
-        if (!(V & 1) && (i & 3) == 3) {
+        if constexpr (RS) {
+          // register staging: piece q of tile t+1 into stage st ^ 1, then tile t+2's piece q into the same registers
+          const int q = 2 * j + (i >> 2);
+          if ((i & 3) == 0) rs_write(st ^ 1, q);
+          if ((i & 3) == 1) rs_load(min(t + 2, nk - 1), q);
+        }
+        if (!(V & 1) && !(V & 2048) && (i & 3) == 3) {   // (V & 2048: lab ablation, no fragment re-reads)
           const int q = 2 * j + (i >> 2);               // 0..15
           if (q < 8) w1[q] = rd(st, wo1, q);
           else x1[q - 8] = rd(st, xo1, q - 8);
@@ -234,9 +270,17 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     constexpr int PRE = (V & 32) ? 12 : (V & 8) ? 8 : 16;
     const int kn = min(t + 2, nk - 1);
     auto dma = [&](int q) {
+      if constexpr ((V & 1024) != 0) return;            // lab ablation: no copies at all (timing only)
+      if constexpr ((V & 4096) != 0) {                   // M0 chained from piece to piece (pieces issued in order)
+        if (q < 7) glds16_chain<1024>(A + (long long)kn * 128, aoff[q]);
+        else if (q == 7) glds16_chain<HG_TILE - 7 * 1024>(A + (long long)kn * 128, aoff[7]);
+        else glds16_chain<1024>(B + (long long)kn * 128, boff[q - 8]);
+        return;
+      }
       if (q < 8) dma_a(kn, st, q);
       else dma_b(kn, st, q - 8);
     };
+    if constexpr (!L && (V & 4096) != 0) hg_set_m0(lds0 + st * HG_STAGE);
     // fragment q of the next step 0, in the order its MFMAs need them (w0[0], x0[0..7], w0[1..7]) unless V & 4 == 0
     auto rdn = [&](int q) {
       if constexpr ((V & 4) != 0) {
@@ -255,6 +299,20 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
         if (((q + 1) * 32) / cnt - 1 == mi) return q;
       return -1;
     };
+    if constexpr (RS) {
+      // register staging: tile t+1 is already in stage st ^ 1 for every wave (half 1's barrier); its step-0
+      // fragments are read under all 64 MFMAs, one per 4
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
+          if constexpr (!L) if ((i & 3) == 3) rdn(2 * j + (i >> 2));
+        }
+        if (!(V & 2)) __builtin_amdgcn_sched_barrier(0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -282,7 +340,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       for (int i = 0; i < 8; ++i) {
         acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
         if constexpr (!L) {
-          if ((i & 1) == 1) rdn(4 * (j - 4) + (i >> 1));       // fragments 0..15
+          if (!(V & 2048) && (i & 1) == 1) rdn(4 * (j - 4) + (i >> 1));       // fragments 0..15
           const int q = piece_at(8 * (j - 4) + i, 16 - PRE);
           if (q >= 0) dma(PRE + q);
         }
@@ -292,22 +350,30 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   };
 
   // ---- prologue: tiles 0 and 1 in flight, tile 0 landed, its step-0 fragments in registers
+  if constexpr (RS) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { dma_a(0, 0, i); dma_b(0, 0, i); }
-  {
+    for (int q = 0; q < 16; ++q) rs_load(0, q);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rs_write(0, q);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rs_load(min(1, nk - 1), q);
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { dma_a(0, 0, i); dma_b(0, 0, i); }
     const int k1 = min(1, nk - 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) { dma_a(k1, 1, i); dma_b(k1, 1, i); }
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
-  __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int f = 0; f < 8; ++f) { w0[f] = rd(0, wo0, f); x0[f] = rd(0, xo0, f); }
 
   half1(std::true_type{}, 0);
   for (int t = 0; t + 1 < nk; ++t) {
     half2(std::false_type{}, t, t & 1);
-    half1(std::false_type{}, (t + 1) & 1);
+    half1(std::false_type{}, t + 1);
   }
   half2(std::true_type{}, nk - 1, (nk - 1) & 1);
   wait_vmcnt0();                                          // no LDS-DMA may outlive the workgroup

@@ -31,3 +31,23 @@ def test_asm_mfma_kernels_compile_spill_free(tmp_path, src, kernel):
             spills.append((names[-1], int(m.group(1))))
     assert spills, "no kernels found"
     assert all(n == 0 for _, n in spills), spills
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
+def test_hgemm_m0_written_only_by_its_dma_statements(tmp_path):
+    """k_hgemm keeps the LDS-DMA destination in M0 across statements (glds16_chain: one s_add per piece).  That is
+    only valid while nothing else in the kernel writes M0: every M0 write in its ISA must be one of the kernel's own
+    forms (s_mov_b32 m0, sN / s_add_u32 m0, m0, imm), and no compiler-inserted M0 save or use may appear."""
+    s = tmp_path / "k.s"
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                        "-ffp-contract=off", "-I", CSRC, os.path.join(CSRC, "hgemm.hip"), "-o", str(s)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    text = s.read_text()
+    bodies = re.findall(r"^(_ZN3bnb7k_hgemm\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.S | re.M)
+    assert bodies, "no k_hgemm kernels"
+    for name, body in bodies:
+        for line in body.splitlines():
+            ins = line.split(";")[0].strip()
+            if re.search(r"\bm0\b", ins):
+                assert re.fullmatch(r"s_mov_b32 m0, s\d+|s_add_u32 m0, m0, (0x[0-9a-f]+|\d+)", ins), (name, ins)

@@ -9,6 +9,7 @@
 #include "hgemm.hip"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -24,6 +25,12 @@ using namespace bnb;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 static float bf2f(uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return f; }
+
+// the k_hgemm schedule variants compared (HG_V bits, csrc/hgemm.hip)
+template <int... Vs> struct Variants {
+  template <class F> static void each(F f) { (f(std::integral_constant<int, Vs>{}), ...); }
+};
+using LabV = Variants<24, 24 + 4096, 8 + 4096, 28 + 4096>;
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096, K = argc > 3 ? atoi(argv[3]) : 11008;
@@ -98,18 +105,19 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     agree(name);
   };
-  check(k_hgemm<HG_BF16, 24>, "hgemm v24");
+  LabV::each([&](auto v) {
+    char name[32];
+    snprintf(name, sizeof name, "hgemm v%d", (int)decltype(v)::value);
+    check(k_hgemm<HG_BF16, decltype(v)::value>, name);
+  });
   const int R = 20;
   for (int r = 0; r < rounds; ++r) {
     const double t_lib = timeit(lib, R);
-    double tv[4];
-    tv[0] = timeit([&] { mine(k_hgemm<HG_BF16, 24>); }, R);
-    tv[1] = timeit([&] { mine(k_hgemm<HG_BF16, 24 + 64>); }, R);
-    tv[2] = timeit([&] { mine(k_hgemm<HG_BF16, 24 + 128>); }, R);
-    tv[3] = timeit([&] { mine(k_hgemm<HG_BF16, 24 + 64 + 128 + 256>); }, R);
     printf("round %d  rocblas %7.1f us %6.0f TF |", r, t_lib, flop / t_lib / 1e6);
-    const int vs[4] = {24, 24 + 64, 24 + 128, 24 + 448};
-    for (int v = 0; v < 4; ++v) printf(" v%d %7.1f us %6.0f TF |", vs[v], tv[v], flop / tv[v] / 1e6);
+    LabV::each([&](auto v) {
+      const double t = timeit([&] { mine(k_hgemm<HG_BF16, decltype(v)::value>); }, R);
+      printf(" v%d %7.1f us %6.0f TF |", (int)decltype(v)::value, t, flop / t / 1e6);
+    });
     printf("\n");
     fflush(stdout);
   }
