@@ -270,8 +270,8 @@ def bench_decode_gemv(dev, iters=30):
 
 def bench_few_token_gemm(dev, iters=30, tokens=(2, 4, 8, 16, 32, 64)):
     """Batched decode / short prefill on the config-2 weight (11008 x 4096 NF4, nested statistics, the
-    Linear4bit default): gemm_4bit with 2..4 activation rows runs the multi-row GEMV (gemv4bit_tok.hip, one
-    launch), 5..64 the weight-streaming MFMA kernel (gemm4bit_skinny.hip, + its ordered split-K reduce).  14 rotating weight copies, HIP-graph replay;
+    Linear4bit default): gemm_4bit with 2..32 activation rows runs the whole-K few-token kernel (gemm4bit_fewtok.hip,
+    one launch), 33..64 the split-K weight-streaming kernel (gemm4bit_skinny.hip, + its ordered reduce).  14 rotating weight copies, HIP-graph replay;
     GB/s over the algorithmic bytes (packed weights + nested stats + activations + output)."""
     n_out, k_in, copies = 11008, 4096, 14
     g = torch.Generator(device=dev).manual_seed(3)
@@ -281,7 +281,8 @@ def bench_few_token_gemm(dev, iters=30, tokens=(2, 4, 8, 16, 32, 64)):
         ws.append(F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True))
         del W
     res = {"shape": [None, n_out, k_in],
-           "path": "2..4 rows: k_gemv_4bit_tok; 5..64 rows: k_gemm_4bit_skinny (+ k_skinny_reduce)"}
+           "path": "2..32 rows: k_gemm_4bit_fewtok (whole K per workgroup, LDS-DMA weight ring, 16x16x32 MFMA, one "
+                   "launch); 33..64 rows: k_gemm_4bit_skinny (+ k_skinny_reduce)"}
     for m in tokens:
         x = torch.randn(m, k_in, device=dev, dtype=torch.bfloat16, generator=g)
         out = torch.empty(m, n_out, device=dev, dtype=torch.bfloat16)

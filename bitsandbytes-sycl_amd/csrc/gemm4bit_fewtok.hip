@@ -1,0 +1,428 @@
+// Few-token 4-bit weight GEMM, whole K per workgroup, one launch (batched decode / short prefill, 1..32 activation
+// rows) for gfx950.
+//
+// Slot and semantics: the M > 1 path of cgemm_4bit_inference (ref:sycl/pythonInterface.cpp:377-378), i.e.
+// dequantize_4bit + F.linear (ref:python_src_quants/autograd/_functions.py:491-507), in the reference GEMV's
+// arithmetic (ref:sycl/sycl_code/kernel_gemm.cpp:1291-1294, 1336-1343: the 16 code values held in T, one absmax per
+// block): each weight contributes T(code[q]) * x in the MFMA (exact fp32 products, fp32 sums over the block's 64 k),
+// and the block sum is scaled by its fp32 absmax (one fp32 fma per output).  Tolerance class: the GEMV's.
+//
+// With a few tokens the product is a weight stream (0.5 B per weight, read once).  What sets the time here
+// (profiles/lab/r03_fewtok32.txt, ablations of the first form of this kernel):
+//   * weight reads in 32-byte pieces of 32 rows per instruction cost ~3 us at 11008 x 4096 against 8 rows x 128 B:
+//     the weights therefore move by LDS-DMA in whole 128-B row segments (4 blocks of 64 k; 16-B slots XOR-swizzled
+//     by (row >> 1) & 7 through the source address) into a per-wave LDS ring, and each lane reads its MFMA operand
+//     bytes from there (ds_read_b64, conflict-free under the swizzle);
+//   * every token / statistics load instruction costs time, so a wave covers TWO 16-row weight groups with each token
+//     fragment (v_mfma_f32_16x16x32: lane (n, g) = (l & 15, l >> 4) holds k = 64b + 16g + 8s .. +7 of MFMA s = 0, 1,
+//     so one 8-B operand read covers exactly one 64-element absmax block b and the block's two MFMAs sum unscaled
+//     T(code) x products; the absmax scale is one fma per accumulator after them -- no per-weight multiply or cast);
+//   * the table maps a packed byte straight to the MFMA operand dword {T(code[hi]), T(code[lo])} (32 bank-private
+//     copies, entry e of copy c at byte 128 e + 4 c: one bit-field extract + one shift-or per lookup);
+//   * tokens are the MFMA A operand (rows = tokens) read straight into registers through a buffer resource over rows
+//     0..M-1 (lanes of rows >= M get an out-of-range offset: zeros, no memory access, no branch).
+// The workgroup (4 waves) owns 16 RG weight rows and all of K; its waves take K in quarters of whole 4-block groups
+// (two groups in flight per wave) and the four partial sums meet in LDS in wave order: deterministic, one launch,
+// no workspace.
+#include "gemm_common.hpp"
+#include "gemv_common.hpp"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace bnb {
+
+// LDS-DMA of a streamed (read-once) 16-B piece per lane: non-temporal, like the GEMV's weight loads (M0 = the
+// wave-uniform LDS base, saved and restored around the statement)
+__device__ __forceinline__ void glds16_nt(const void* gsrc, void* lds_base) {
+  unsigned keep;
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_base);
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
+}
+
+constexpr int FT_THREADS = 256;
+constexpr int FT_TABLE = 256 * 128;     // 32 copies x 256 entries x 4 B
+constexpr int FT_NG = 2;                // 4-block groups in flight per wave
+
+template <typename T> struct FtMfma;
+template <> struct FtMfma<bf16_t> {
+  __device__ static __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                   0, 0, 0);
+  }
+};
+template <> struct FtMfma<fp16_t> {
+  __device__ static __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                  0, 0);
+  }
+};
+
+template <int RG, int WAVES> constexpr int ft_lds_bytes() { return FT_TABLE + 1024 + WAVES * FT_NG * (16 * RG * 128); }
+
+// RG: 16-row weight groups per workgroup (and per wave); MT: 16-token A tiles (1: <= 16 tokens, 2: <= 32).
+// S4: blocksize 64 with K % 256 == 0 (and a nested group of >= 4 blocks): the four statistics of a row's group are
+// contiguous and aligned, so they arrive as ONE load per row group (plain: float4; nested: 4 codes as a dword + one
+// absmax2) instead of one or two per block -- per-block statistics loads were the largest cost of the first form
+// (profiles/lab/r03_fewtok32.txt).
+// ABL (lab ablations, wrong results, timing only): 1 = no token loads, 2 = no statistics loads, 4 = no table lookups;
+// 32 = the weight DMA without the non-temporal hint (correct results).
+// WAVES: the workgroup's waves, each a 1 / WAVES share of K (whole 4-block groups); one workgroup per CU.
+template <typename T, int RG, int MT, bool NESTED, bool S4, int WAVES, int ABL = 0>
+__global__ void __launch_bounds__(64 * WAVES, 1)
+k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
+                   SkStats st, const float* __restrict__ code, T* __restrict__ out, int ldc) {
+  constexpr int ROWS = 16 * RG;
+  constexpr int GB = ROWS * 128;                            // LDS bytes of one group: ROWS rows x 4 blocks x 32 B
+  constexpr int PIECES = ROWS / 8;                          // 1-KiB DMA pieces per group (8 rows x 128 B each)
+  constexpr int NV = RG * MT;                               // accumulator tiles per lane
+  // VMEM instructions of one group, in issue order: tokens, statistics, then the DMA pieces
+  constexpr int GROUP_OPS =
+      ((ABL & 1) ? 0 : 4 * MT * 2) + ((ABL & 2) ? 0 : (S4 ? 1 : 4) * RG * (NESTED ? 2 : 1)) + PIECES;
+  __shared__ __attribute__((aligned(16))) uint8_t sm[ft_lds_bytes<RG, WAVES>()];
+  uint8_t* table = sm;
+  float* code2s = reinterpret_cast<float*>(sm + FT_TABLE);
+  uint8_t* ring = sm + FT_TABLE + 1024;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * ROWS;
+  const int nblk = K >> 6, ngr = (nblk + 3) >> 2;            // 64-k blocks; 4-block groups
+  const int g0 = wave * ngr / WAVES, ng = (wave + 1) * ngr / WAVES - g0;   // this wave's groups (may be 0)
+  const int rowbytes = K >> 1;
+
+  // ---- table values first (the VMEM counter retires in order)
+  const int te = tid & 255;                                 // table entry of this thread (tid < 256 stores it)
+  const float code_hi = code[te >> 4], code_lo = code[te & 15];
+  float offset = 0.0f, c2v = 0.0f;
+  if constexpr (NESTED) {
+    c2v = st.code2[te];
+    offset = *st.offset;
+  }
+  asm volatile("" ::: "memory");
+
+  // ---- per-lane sources
+  // tokens: A tile mt, lane (t = n, g): row 16 mt + n, elements 64 b + 16 g + 8 s .. +7 (s = 0, 1: 32 contiguous bytes)
+  const uint32_t xbytes = (uint32_t)(((long long)(M - 1) * lda + K) * sizeof(T));
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(A), (short)0, (int)xbytes, 0x00020000);
+  uint32_t xoff[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int t = 16 * mt + n;
+    xoff[mt] = t < M ? (uint32_t)(((long long)t * lda + 16 * g) * sizeof(T)) : 0x80000000u;
+  }
+  // statistics: weight row r0 + 16 rg + n (clamped), element index of block b = 2 ldb row + 64 b
+  long long sbase[RG];
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg) sbase[rg] = 2LL * ldb * min(r0 + 16 * rg + n, N - 1);
+  // DMA: piece j of a group = rows 8j .. 8j+7; lane l -> row 8j + (l >> 3), LDS slot l & 7 holding source slot
+  // (l & 7) ^ ((row >> 1) & 7); slots past the row's end (the last, partial group) re-read its last slot (never used)
+  const uint8_t* wsrc[PIECES];
+  int wslot[PIECES];
+#pragma unroll
+  for (int j = 0; j < PIECES; ++j) {
+    const int rr = 8 * j + (lane >> 3);
+    wslot[j] = 16 * ((lane & 7) ^ ((rr >> 1) & 7));
+    wsrc[j] = B + (long long)min(r0 + rr, N - 1) * ldb;
+  }
+  uint8_t* my_ring = ring + wave * FT_NG * GB;
+
+  struct Group {
+    uint4 x[4][MT][2];
+    float am[S4 ? 1 : 4][RG];
+    uint32_t q8[S4 ? 1 : 4][RG];
+    float a2[S4 ? 1 : 4][RG];
+    float4 am4[S4 ? RG : 1];                                // S4: the group's statistics as loaded (unpacked in use)
+    uint32_t q4[S4 ? RG : 1];
+    float a2g[S4 ? RG : 1];
+  };
+  Group gr[FT_NG];
+  auto issue = [&](Group& R, int gi, int slot) {            // this wave's group gi into ring slot `slot`
+    const int ga = g0 + gi;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int b = min(4 * ga + bb, nblk - 1);
+      if constexpr ((ABL & 1) == 0) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(xoff[mt] + (uint32_t)(128 * b + 16 * s)), 0, 0);
+            R.x[bb][mt][s] = make_uint4(v[0], v[1], v[2], v[3]);
+          }
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) R.x[bb][mt][0] = R.x[bb][mt][1] = make_uint4(b, mt, 0, 0);
+      }
+      if constexpr ((ABL & 2) == 0 && !S4) {
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) {
+          const long long j = (sbase[rg] + 64LL * b) >> st.bs_shift;
+          if constexpr (NESTED) {
+            R.q8[bb][rg] = st.q8[j];
+            R.a2[bb][rg] = st.absmax2[j >> st.bs2_shift];
+          } else {
+            R.am[bb][rg] = st.absmax[j];
+          }
+        }
+      } else if constexpr ((ABL & 2) != 0 && !S4) {
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) { R.q8[bb][rg] = 1; R.a2[bb][rg] = 1.f; R.am[bb][rg] = 1.f; }
+      }
+    }
+    if constexpr ((ABL & 2) != 0 && S4) {
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) { R.q4[rg] = 0x01010101u; R.a2g[rg] = 1.f; R.am4[rg] = make_float4(1.f, 1.f, 1.f, 1.f); }
+    }
+    if constexpr ((ABL & 2) == 0 && S4) {                  // the group's 4 statistics per row in one load
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        const long long j0 = (sbase[rg] >> 6) + 4LL * min(ga, ngr - 1);
+        if constexpr (NESTED) {
+          R.q4[rg] = *reinterpret_cast<const uint32_t*>(st.q8 + j0);
+          R.a2g[rg] = st.absmax2[j0 >> st.bs2_shift];
+        } else {
+          R.am4[rg] = *reinterpret_cast<const float4*>(st.absmax + j0);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // this slot's previous ring reads are done (WAR)
+    const int col = 128 * ga;
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) {
+      if constexpr ((ABL & 32) != 0) glds16(wsrc[j] + min(col + wslot[j], rowbytes - 16), my_ring + slot * GB + 1024 * j);
+      else glds16_nt(wsrc[j] + min(col + wslot[j], rowbytes - 16), my_ring + slot * GB + 1024 * j);
+    }
+  };
+  auto wait_group = [&](bool next_issued) {                 // the oldest group in flight has landed (DMA included)
+    if (next_issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GROUP_OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  // both prologue groups unconditionally (clamped: a wave with fewer groups re-reads its last one, never consumed) --
+  // a branch here would make hipcc's wait for the table values above conservative (vmcnt(0) behind the stream)
+  issue(gr[0], 0, 0);
+  issue(gr[1], min(1, max(ng - 1, 0)), 1);
+
+  // ---- table: thread t writes entry t = {T(code[t >> 4]), T(code[t & 15])} into its 32 copies
+  if (tid < 256) {
+    const int t = tid;
+    const uint32_t v = Dot2<T>::pair(code_hi, code_lo);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 128 * t + 16 * ((k + t) & 7)) = make_uint4(v, v, v, v);
+    if constexpr (NESTED) code2s[t] = c2v;
+  }
+  __syncthreads();
+
+  const uint32_t lane4 = (uint32_t)(lane & 31) * 4;
+  f32x4_t acc[RG][MT];
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[rg][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto consume = [&](const Group& R, int gi, int slot) {
+    const uint8_t* gs = my_ring + slot * GB;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      if (4 * (g0 + gi) + bb >= nblk) break;                 // (wave-uniform) the partial last group
+      // this lane's 8 packed bytes of block bb: row 16 rg + n, bytes 32 bb + 8 g .. +7 = 16-B slot 2 bb + (g >> 1)
+      uint2 wv[RG];
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        const int rr = 16 * rg + n;
+        const int slot16 = (2 * bb + (g >> 1)) ^ ((rr >> 1) & 7);
+        wv[rg] = *reinterpret_cast<const uint2*>(gs + rr * 128 + 16 * slot16 + 8 * (g & 1));
+      }
+      f32x4_t blk[RG][MT];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) {
+          const uint32_t d = s ? wv[rg].y : wv[rg].x;
+          uint32_t l[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {                      // byte i -> entry, lane copy -> bank
+            if constexpr ((ABL & 4) != 0) l[i] = d + i;
+            else l[i] = *reinterpret_cast<const uint32_t*>(table + ((__builtin_amdgcn_ubfe(d, 8 * i, 8) << 7) | lane4));
+          }
+          const uint4 bf = make_uint4(l[0], l[1], l[2], l[3]);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            blk[rg][mt] = FtMfma<T>::mma(R.x[bb][mt][s], bf, s ? blk[rg][mt] : f32x4_t{0.f, 0.f, 0.f, 0.f});
+        }
+      }
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        float a;
+        if constexpr (S4) {
+          if constexpr (NESTED) a = __fadd_rn(__fmul_rn(code2s[(R.q4[rg] >> (8 * bb)) & 0xFF], R.a2g[rg]), offset);
+          else a = bb == 0 ? R.am4[rg].x : bb == 1 ? R.am4[rg].y : bb == 2 ? R.am4[rg].z : R.am4[rg].w;
+        } else {
+          if constexpr (NESTED) a = __fadd_rn(__fmul_rn(code2s[R.q8[bb][rg]], R.a2[bb][rg]), offset);
+          else a = R.am[bb][rg];
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[rg][mt][i] = __builtin_fmaf(a, blk[rg][mt][i], acc[rg][mt][i]);
+      }
+    }
+  };
+
+  // ---- main loop: group gi in slot gi & 1; group gi + 2 refills that slot once gi is consumed
+  int gi = 0;
+  for (; gi + 3 < ng; gi += 2) {                            // steady state: both refills in range, no branches
+    wait_group(true);
+    consume(gr[0], gi, 0);
+    issue(gr[0], gi + 2, 0);
+    wait_group(true);
+    consume(gr[1], gi + 1, 1);
+    issue(gr[1], gi + 3, 1);
+  }
+  // tail: groups gi .. ng - 1 (at most 3), wave-uniform branches
+  if (gi < ng) {
+    wait_group(gi + 1 < ng);
+    consume(gr[0], gi, 0);
+    if (gi + 2 < ng) issue(gr[0], gi + 2, 0);
+  }
+  if (gi + 1 < ng) {
+    wait_group(gi + 2 < ng);
+    consume(gr[1], gi + 1, 1);
+  }
+  if (gi + 2 < ng) {
+    wait_group(false);
+    consume(gr[0], gi + 2, 0);
+  }
+
+  // ---- the WAVES K shares meet in LDS, summed in wave order
+  __syncthreads();                                          // every wave is done with the table and its ring
+  float* red = reinterpret_cast<float*>(sm);
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[((wave * NV + rg * MT + mt) * 4 + i) * 64 + lane] = acc[rg][mt][i];
+  __syncthreads();
+  // D[4 g + i][n] of tile (rg, mt): token 16 mt + 4 g + i, weight row r0 + 16 rg + n
+  for (int v = wave; v < NV * 4; v += WAVES) {
+    const int tile = v >> 2, i = v & 3, rg = tile / MT, mt = tile - rg * MT;
+    float s = red[v * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) s += red[(w * NV * 4 + v) * 64 + lane];
+    const int t = 16 * mt + 4 * g + i, col = r0 + 16 * rg + n;
+    if (t < M && col < N) out[(long long)t * ldc + col] = Io<T>::from_f32(s);
+  }
+}
+
+// 0 = auto, 1 = off, 2 = forced wherever it fits (A/B knob; tests); >= 16: lab ablations
+int g_fewtok_mode = 0;
+extern int g_fewtoken_kernel;   // gemm4bit_wk.hip: != 0 selects one of the older few-token kernels
+
+bool fewtok_applicable(int m, int n, int k, int lda, int ldb, int blocksize, const void* A, const void* B) {
+  return g_fewtok_mode != 1 && n >= 1 && n <= 32 && m >= 1 && k >= 64 && k % 64 == 0 && 2LL * ldb >= k &&
+         blocksize >= 64 && (blocksize & (blocksize - 1)) == 0 && lda % 8 == 0 && ldb % 16 == 0 &&
+         ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
+         (long long)(n - 1) * lda * 2 + 2LL * k < 0x7FFFFFFFLL;
+}
+
+int fewtok_rows_groups(int m) {                           // RG: 16-row groups per workgroup (one workgroup per CU)
+  const int cus = device_cu_count();
+  return std::min(4, std::max(1, (m + 16 * cus - 1) / (16 * cus)));
+}
+
+// The auto rule (tools/fewtok32_ab.py, profiles/lab/r03_fewtok32.txt; 11008 x 4096 at 8 tokens 17.2 -> 10.2 us,
+// 4096 x 4096 10.5 -> 5.9 us, 2..4 rows ahead of the multi-row GEMV): weights of >= 3/4 of a 16-row group per CU;
+// at 17..32 tokens only with >= 2 row groups per workgroup (one 16-row group re-reads each token fragment for too few
+// weights: 4096 x 11008 at 32 tokens 24.7 vs 21.8 us split-K); at 2..4 tokens not on the 4-wave 64-row form
+// (14336 x 4096 at 2 tokens 15.0 vs 12.0 us multi-row GEMV).
+bool fewtok_auto_takes(int m, int n, int k) {
+  const int cus = device_cu_count(), rg = fewtok_rows_groups(m);
+  if (4 * ((m + 15) / 16) < 3 * cus) return false;
+  if (n > 16 && rg < 2) return false;
+  if (n <= 4 && rg >= 4) return false;
+  return true;
+}
+
+// m = out features (weight rows), n = tokens, k = in features.  False: not applicable (nothing launched).
+template <typename T>
+bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
+                             int blocksize, int blocksize2, const float* code, T* out, int ldc) {
+  if (!fewtok_applicable(m, n, k, lda, ldb, blocksize, A, B)) return false;
+  const bool nested = st.q8 != nullptr;
+  if (nested && (blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1)))) return false;
+  if (g_fewtok_mode == 0 && !fewtok_auto_takes(m, n, k)) return false;
+  // one workgroup per CU: RG 16-row groups each, as few as cover the rows in one round (11008 rows: 3 -> 230
+  // workgroups); 8 waves (two per SIMD) where the LDS ring allows it, else 4
+  const int rg = fewtok_rows_groups(m);
+  st.bs_shift = __builtin_ctz(blocksize);
+  st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
+  const dim3 grid((unsigned)((m + 16 * rg - 1) / (16 * rg)));
+  // the 4-statistics-per-load form: blocksize 64, whole 4-block groups per row (K % 256 == 0, so every row's first
+  // statistic is 4-aligned), a nested group of >= 4 blocks
+  const bool s4 = blocksize == 64 && k % 256 == 0 && (2LL * ldb) % 256 == 0 && (!nested || blocksize2 >= 4);
+  auto go = [&](auto kern, int waves) {
+    hipLaunchKernelGGL(kern, grid, dim3(64 * waves), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc);
+  };
+  if (g_fewtok_mode >= 16) {                                // lab ablations: nested, <= 16 tokens, 48-row workgroups
+    if (!nested || n > 16 || rg != 3 || !s4) return false;
+    switch (g_fewtok_mode - 16) {
+      case 1: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 1>, 8); break;
+      case 2: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 2>, 8); break;
+      case 3: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 3>, 8); break;
+      case 4: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 4>, 8); break;
+      case 7: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 7>, 8); break;
+      case 32: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 32>, 8); break;
+      case 39: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 39>, 8); break;
+      default: return false;
+    }
+    return true;
+  }
+  auto by_rg = [&](auto mt_tag, auto nested_tag, auto s4_tag) {
+    constexpr int MT = decltype(mt_tag)::value;
+    constexpr bool NS = decltype(nested_tag)::value, S = decltype(s4_tag)::value;
+    switch (rg) {
+      case 1: go(k_gemm_4bit_fewtok<T, 1, MT, NS, S, 8>, 8); break;
+      case 2: go(k_gemm_4bit_fewtok<T, 2, MT, NS, S, 8>, 8); break;
+      case 3:   // (17..32 tokens with per-block statistics: 4 waves, 8 would spill)
+        if constexpr (MT == 2 && !S) go(k_gemm_4bit_fewtok<T, 3, MT, NS, S, 4>, 4);
+        else go(k_gemm_4bit_fewtok<T, 3, MT, NS, S, 8>, 8);
+        break;
+      default: go(k_gemm_4bit_fewtok<T, 4, MT, NS, S, 4>, 4); break;
+    }
+  };
+  auto by_s4 = [&](auto mt_tag, auto nested_tag) {
+    if (s4) by_rg(mt_tag, nested_tag, std::true_type{});
+    else by_rg(mt_tag, nested_tag, std::false_type{});
+  };
+  auto by_tokens = [&](auto nested_tag) {
+    if (n <= 16) by_s4(std::integral_constant<int, 1>{}, nested_tag);
+    else by_s4(std::integral_constant<int, 2>{}, nested_tag);
+  };
+  if (nested) by_tokens(std::true_type{});
+  else by_tokens(std::false_type{});
+  return true;
+}
+
+template bool launch_gemm_4bit_fewtok<bf16_t>(int, int, int, const bf16_t*, int, const uint8_t*, int, SkStats, int, int,
+                                              const float*, bf16_t*, int);
+template bool launch_gemm_4bit_fewtok<fp16_t>(int, int, int, const fp16_t*, int, const uint8_t*, int, SkStats, int, int,
+                                              const float*, fp16_t*, int);
+
+}  // namespace bnb
+
+extern "C" {
+// [additive, testing] whole-K few-token kernel: 0 = auto, 1 = off, 2 = wherever it fits
+void cgemm_4bit_set_fewtok_mode(int mode) { bnb::g_fewtok_mode = mode; }
+// [additive] 1 when the 4-bit GEMM entry points run the whole-K few-token kernel for out features m, n activation rows,
+// in features k and this blocksize (the auto rule above, or the forced mode), else 0 -- the Python layer asks before
+// it sends 2..4 rows to the multi-row GEMV
+int cgemm_4bit_fewtok_takes(int m, int n, int k, int blocksize) {
+  if (bnb::g_fewtok_mode == 1 || bnb::g_fewtoken_kernel != 0 || n < 1 || n > 32 || k < 64 || k % 64 || blocksize < 64 || (blocksize & (blocksize - 1)))
+    return 0;
+  return (bnb::g_fewtok_mode >= 2 || bnb::fewtok_auto_takes(m, n, k)) ? 1 : 0;
+}
+}

@@ -281,6 +281,7 @@ bool skinny_applicable(int m, int n, int k, int lda, int ldb, int blocksize, con
 // that round is at least 70 % full.  At 1..32 rows the 8-wave forms lost everywhere (same NB: +1..3 us; 2 x NB: +5..14 us).
 // g_skinny_cfg (cgemm_4bit_set_skinny_config, lab A/B): -1 = that rule, 0 = base, 1 = 8 waves same NB, 2 = 8 waves 2 x NB.
 static int g_skinny_cfg = -1;
+extern int g_fewtoken_kernel;   // gemm4bit_wk.hip
 
 struct SkGeom {
   int cfg, waves, nb, splits;
@@ -318,6 +319,10 @@ template <typename T>
 bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
                              int blocksize, int blocksize2, const float* code, T* out, int ldc, float* ws,
                              long long ws_bytes) {
+  // the whole-K MFMA kernel first (gemm4bit_fewtok.hip), unless a lab / test knob selects one of the older kernels
+  if (g_fewtoken_kernel == 0 && g_skinny_cfg < 0 &&
+      launch_gemm_4bit_fewtok<T>(m, n, k, A, lda, B, ldb, st, blocksize, blocksize2, code, out, ldc))
+    return true;
   if (launch_gemm_4bit_wk<T>(m, n, k, A, lda, B, ldb, st, blocksize, blocksize2, code, out, ldc)) return true;
   if (!skinny_applicable(m, n, k, lda, ldb, blocksize, A, B)) return false;
   const bool nested = st.q8 != nullptr;

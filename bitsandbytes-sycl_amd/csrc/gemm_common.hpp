@@ -98,6 +98,12 @@ bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uin
                              int blocksize, int blocksize2, const float* code, T* out, int ldc, float* ws,
                              long long ws_bytes);
 
+// Few-token kernel on the 32x32x16 MFMA, whole K per workgroup, no workspace (gemm4bit_fewtok.hip): 1..32 activation
+// rows, K % 64 == 0, K >= 256.  False when the shape / alignment does not fit (nothing launched).
+template <typename T>
+bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
+                             int blocksize, int blocksize2, const float* code, T* out, int ldc);
+
 // Few-token kernel with whole K per workgroup (gemm4bit_wk.hip): 1..32 activation rows, K % 128 == 0, no workspace.
 // False when the shape / alignment does not fit or the A/B knob selects the skinny kernel.
 template <typename T>

@@ -47,7 +47,7 @@ class BNBNativeLibrary:
                      "cdequantize_blockwise_nested_fp16_fp4", "cdequantize_blockwise_nested_fp16_nf4",
                      "cdequantize_blockwise_nested_bf16_fp4", "cdequantize_blockwise_nested_bf16_nf4",
                      "cint8_row_quant_fp16", "cgemm_4bit_inference_nested_ws_bf16",
-                     "cgemm_4bit_inference_nested_ws_fp16", "cset_cpu_threads"):
+                     "cgemm_4bit_inference_nested_ws_fp16", "cset_cpu_threads", "cgemm_4bit_fewtok_takes"):
             getattr(lib, name).restype = ct.c_int
 
     def __getattr__(self, item):

@@ -910,6 +910,27 @@ def _dequant_workspace(device, dtype, numel: int) -> Tensor:
     return ws[:numel]
 
 
+@functools.lru_cache(maxsize=4096)
+def _fewtok_takes_cached(mode: int, n: int, rows: int, k: int, blocksize: int) -> bool:
+    return bool(lib.cgemm_4bit_fewtok_takes(ct.c_int32(n), ct.c_int32(rows), ct.c_int32(k), ct.c_int32(blocksize)))
+
+
+def _fewtok_takes(n: int, rows: int, k: int, blocksize: int) -> bool:
+    """Whether the C side runs the whole-K few-token kernel (gemm4bit_fewtok.hip) for this shape; 2..4 rows then go
+    there instead of the multi-row GEMV (measured faster wherever its rule takes the shape, profiles/lab/r03_fewtok32.txt).
+    Cached per shape and the kernel's test knob (cgemm_4bit_set_fewtok_mode, mirrored in _FEWTOK_MODE)."""
+    return _fewtok_takes_cached(_FEWTOK_MODE[0], n, rows, k, blocksize)
+
+
+_FEWTOK_MODE = [0]
+
+
+def set_fewtok_mode(mode: int) -> None:
+    """Test / A-B knob of the whole-K few-token kernel: 0 = auto, 1 = off, 2 = wherever it fits."""
+    lib.cgemm_4bit_set_fewtok_mode(ct.c_int(mode))
+    _FEWTOK_MODE[0] = mode
+
+
 def _gemm_4bit_tokens(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor],
                       events: Optional[list]) -> bool:
     """2..GEMM_4BIT_GEMV_TOKENS rows through cgemm_4bit_inference_tokens_* (one launch; compressed statistics
@@ -978,7 +999,8 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         if measured is not None:
             route = measured
     library = route in ("library", "library_tn", "hgemm")
-    if not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events):
+    if (not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and not _fewtok_takes(N, rows, K, state.blocksize)
+            and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events)):
         return out.view(*A.shape[:-1], N)
     if (absmax is None and not library and rows <= GEMM_4BIT_FEW_TOKENS and _nested_stats_in_kernel_ok(state)):
         # few tokens, compressed statistics: one launch of the weight-streaming kernel that decodes the

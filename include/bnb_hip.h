@@ -92,6 +92,13 @@ int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bnb_bf16* A, uns
  * 1 = the split-K kernel (gemm4bit_skinny.hip + its ordered reduce) only, 2 = the whole-K kernel wherever it fits */
 void cgemm_4bit_set_fewtoken_kernel(int which);
 
+/* [additive, testing] the whole-K few-token kernel (gemm4bit_fewtok.hip; 1..32 activation rows, LDS-DMA weight ring,
+ * 16x16x32 MFMA, tried before the kernels above): 0 = auto (where its shape rule takes it), 1 = off, 2 = wherever it fits */
+void cgemm_4bit_set_fewtok_mode(int mode);
+/* [additive] 1 when the 4-bit GEMM entry points (cgemm_4bit_inference*, the few-token ws / nested entries) run that
+ * kernel for m out features, n activation rows, k in features and this blocksize, else 0 */
+int cgemm_4bit_fewtok_takes(int m, int n, int k, int blocksize);
+
 /* [additive, testing] GEMV kernel choice: 0 = auto (the balanced-range kernel where the shape fits, else the
  * 4-waves-x-R-rows kernel), 1 = the 4-waves-x-R-rows kernel only; both give identical bits */
 void cgemv_4bit_set_kernel(int which);

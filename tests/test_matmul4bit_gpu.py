@@ -647,7 +647,11 @@ def test_gemm_4bit_multirow_gemv_matches_gemv(dev, dtype, nested, rows, shape):
     W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
     X = torch.randn(rows, K, device=dev, dtype=dtype)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
-    Y = F.gemm_4bit(X, q, st)
+    F.set_fewtok_mode(1)                       # the multi-row GEMV itself (the whole-K MFMA kernel takes these by default)
+    try:
+        Y = F.gemm_4bit(X, q, st)
+    finally:
+        F.set_fewtok_mode(0)
     assert Y.shape == (rows, N)
     F.lib.cgemv_4bit_set_kernel(3)              # the balanced / dot GEMV family (not the wide kernel of narrow weights)
     try:
@@ -674,7 +678,11 @@ def test_gemm_4bit_multirow_gemv_vs_oracle(dev, nested, qt, bs, mnk):
     W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
-    Y = F.gemm_4bit(X, q, st)
+    F.set_fewtok_mode(1)                       # the multi-row GEMV itself
+    try:
+        Y = F.gemm_4bit(X, q, st)
+    finally:
+        F.set_fewtok_mode(0)
     absmax = F._absmax_fp32(st).cpu().numpy()
     exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, bs,
                                     st.code.cpu().numpy(), "bf16")
@@ -825,3 +833,43 @@ def test_library_gemm_solution_search(dev, dtype, mnk):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(Y2, _lib_matmul(F, X2, Wd))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("qt,bs", [("nf4", 64), ("fp4", 64), ("nf4", 256)])
+@pytest.mark.parametrize("mnk", [(1, 4096, 4096), (2, 11008, 4096), (5, 1001, 2048), (8, 4096, 11008),
+                                 (13, 300, 1152), (16, 8192, 256), (17, 520, 640), (32, 11008, 4096), (31, 63, 11008),
+                                 (3, 14336, 4096), (24, 14337, 1024), (9, 8200, 768)])
+def test_fewtok32_kernel_vs_oracle(dev, dtype, nested, qt, bs, mnk):
+    """The whole-K few-token kernel (gemm4bit_fewtok.hip), forced wherever it fits (set_fewtok_mode(2), the 2..4-row
+    GEMV switched off): 1..4 row groups per workgroup (1001 .. 11008 out features), 4- and 8-wave forms, ragged out
+    features, K shares of unequal length (K = 11008: 43 groups; 640: a partial 4-block group, waves without groups),
+    the per-block and the 4-per-load statistics forms (blocksize 256 / 64), FP4, nested and plain statistics --
+    against the fp64 oracle.  Its arithmetic is the reference GEMV's (T(code) * x summed per block, then * absmax), so
+    the bar is the GEMV's / the tile kernels'."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M * 13 + N + bs)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
+    saved = F.GEMM_4BIT_GEMV_TOKENS
+    F.GEMM_4BIT_GEMV_TOKENS = 1
+    F.set_fewtok_mode(2)
+    try:
+        Y = F.gemm_4bit(X, q, st)
+        Y2 = F.gemm_4bit(X, q, st)
+        Yp = F.gemm_4bit(X, q, st, absmax=F._absmax_fp32(st))
+    finally:
+        F.set_fewtok_mode(0)
+        F.GEMM_4BIT_GEMV_TOKENS = saved
+    assert Y.shape == (M, N) and Y.dtype == dtype
+    assert torch.equal(Y, Y2)                          # deterministic (the K quarters meet in wave order)
+    assert torch.equal(Y, Yp)                          # in-kernel nested decode = the decoded absmax passed in
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, bs,
+                                    st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
+    assert frac == 0.0, err
