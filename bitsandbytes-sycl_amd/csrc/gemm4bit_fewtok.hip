@@ -41,6 +41,14 @@ __device__ __forceinline__ void glds16_nt(const void* gsrc, void* lds_base) {
                : "=&s"(keep) : "v"(gsrc), "s"(dst) : "memory");
 }
 
+// lab timeline (ABL 128): per wave 8 s_memrealtime stamps (10 ns ticks) at g_ft_tl[(block * 8 + wave) * 8 + i]
+__device__ unsigned long long* g_ft_tl = nullptr;
+__device__ __forceinline__ unsigned long long ft_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 constexpr int FT_THREADS = 256;
 constexpr int FT_TABLE = 256 * 128;     // 32 copies x 256 entries x 4 B
 constexpr int FT_NG = 2;                // 4-block groups in flight per wave
@@ -67,9 +75,14 @@ template <int RG, int WAVES> constexpr int ft_lds_bytes() { return FT_TABLE + 10
 // absmax2) instead of one or two per block -- per-block statistics loads were the largest cost of the first form
 // (profiles/lab/r03_fewtok32.txt).
 // ABL (lab ablations, wrong results, timing only): 1 = no token loads, 2 = no statistics loads, 4 = no table lookups;
-// 32 = the weight DMA without the non-temporal hint (correct results).
+// 32 = the weight DMA without the non-temporal hint (correct results); 64 = the weight pieces loaded into registers
+// (non-temporal) instead of the ring (its reads see stale data); 128 = per-wave timeline stamps (g_ft_tl, lab).
 // WAVES: the workgroup's waves, each a 1 / WAVES share of K (whole 4-block groups); one workgroup per CU.
-template <typename T, int RG, int MT, bool NESTED, bool S4, int WAVES, int ABL = 0>
+// X8 (<= 8 tokens, MT 1): the A operand's rows 8..15 are dead, so ONE token load per lane fetches two blocks -- lanes
+// t < 8 block b of row t, lanes t >= 8 block b + 1 of row t - 8 -- and block b + 1's fragment is brought down to
+// lanes t < 8 by a DPP row rotate (4 v_mov_dpp): half the token load instructions, which the per-CU vector-memory
+// issue rate makes worth more than the moves (profiles/lab/r03_fewtok32_timeline.txt).
+template <typename T, int RG, int MT, bool NESTED, bool S4, int WAVES, bool X8 = false, int ABL = 0>
 __global__ void __launch_bounds__(64 * WAVES, 1)
 k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
                    SkStats st, const float* __restrict__ code, T* __restrict__ out, int ldc) {
@@ -78,8 +91,9 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
   constexpr int PIECES = ROWS / 8;                          // 1-KiB DMA pieces per group (8 rows x 128 B each)
   constexpr int NV = RG * MT;                               // accumulator tiles per lane
   // VMEM instructions of one group, in issue order: tokens, statistics, then the DMA pieces
+  static_assert(!X8 || MT == 1, "X8: one 16-token tile");
   constexpr int GROUP_OPS =
-      ((ABL & 1) ? 0 : 4 * MT * 2) + ((ABL & 2) ? 0 : (S4 ? 1 : 4) * RG * (NESTED ? 2 : 1)) + PIECES;
+      ((ABL & 1) ? 0 : (X8 ? 2 : 4) * MT * 2) + ((ABL & 2) ? 0 : (S4 ? 1 : 4) * RG * (NESTED ? 2 : 1)) + PIECES;
   __shared__ __attribute__((aligned(16))) uint8_t sm[ft_lds_bytes<RG, WAVES>()];
   uint8_t* table = sm;
   float* code2s = reinterpret_cast<float*>(sm + FT_TABLE);
@@ -92,6 +106,8 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
   const int nblk = K >> 6, ngr = (nblk + 3) >> 2;            // 64-k blocks; 4-block groups
   const int g0 = wave * ngr / WAVES, ng = (wave + 1) * ngr / WAVES - g0;   // this wave's groups (may be 0)
   const int rowbytes = K >> 1;
+  unsigned long long tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr ((ABL & 128) != 0) tl[0] = ft_now();
 
   // ---- table values first (the VMEM counter retires in order)
   const int te = tid & 255;                                 // table entry of this thread (tid < 256 stores it)
@@ -110,8 +126,13 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
   uint32_t xoff[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int t = 16 * mt + n;
-    xoff[mt] = t < M ? (uint32_t)(((long long)t * lda + 16 * g) * sizeof(T)) : 0x80000000u;
+    if constexpr (X8) {
+      const int t = n & 7;
+      xoff[mt] = t < M ? (uint32_t)(((long long)t * lda + 16 * g + 64 * (n >> 3)) * sizeof(T)) : 0x80000000u;
+    } else {
+      const int t = 16 * mt + n;
+      xoff[mt] = t < M ? (uint32_t)(((long long)t * lda + 16 * g) * sizeof(T)) : 0x80000000u;
+    }
   }
   // statistics: weight row r0 + 16 rg + n (clamped), element index of block b = 2 ldb row + 64 b
   long long sbase[RG];
@@ -134,6 +155,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     float am[S4 ? 1 : 4][RG];
     uint32_t q8[S4 ? 1 : 4][RG];
     float a2[S4 ? 1 : 4][RG];
+    uint4 wd[(ABL & 64) ? PIECES : 1];                      // (lab ABL 64: the weight pieces in registers)
     float4 am4[S4 ? RG : 1];                                // S4: the group's statistics as loaded (unpacked in use)
     uint32_t q4[S4 ? RG : 1];
     float a2g[S4 ? RG : 1];
@@ -144,7 +166,15 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       const int b = min(4 * ga + bb, nblk - 1);
-      if constexpr ((ABL & 1) == 0) {
+      if constexpr ((ABL & 1) == 0 && X8) {
+        if ((bb & 1) == 0) {                               // blocks bb, bb + 1 in one load (rows 0..7 / lanes 8..15)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(xoff[0] + (uint32_t)(128 * b + 16 * s)), 0, 0);
+            R.x[bb][0][s] = make_uint4(v[0], v[1], v[2], v[3]);
+          }
+        }
+      } else if constexpr ((ABL & 1) == 0) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -192,19 +222,28 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     const int col = 128 * ga;
 #pragma unroll
     for (int j = 0; j < PIECES; ++j) {
-      if constexpr ((ABL & 32) != 0) glds16(wsrc[j] + min(col + wslot[j], rowbytes - 16), my_ring + slot * GB + 1024 * j);
+      if constexpr ((ABL & 64) != 0) {
+        const u32x4_t v = __builtin_nontemporal_load((gvec_p)(wsrc[j] + min(col + wslot[j], rowbytes - 16)));
+        R.wd[j] = make_uint4(v.x, v.y, v.z, v.w);
+      } else if constexpr ((ABL & 32) != 0) glds16(wsrc[j] + min(col + wslot[j], rowbytes - 16), my_ring + slot * GB + 1024 * j);
       else glds16_nt(wsrc[j] + min(col + wslot[j], rowbytes - 16), my_ring + slot * GB + 1024 * j);
     }
   };
+  int nwait = 0;
   auto wait_group = [&](bool next_issued) {                 // the oldest group in flight has landed (DMA included)
     if (next_issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GROUP_OPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr ((ABL & 128) != 0) {
+      if (nwait < 3) tl[3 + nwait] = ft_now();
+      ++nwait;
+    }
   };
 
   // both prologue groups unconditionally (clamped: a wave with fewer groups re-reads its last one, never consumed) --
   // a branch here would make hipcc's wait for the table values above conservative (vmcnt(0) behind the stream)
   issue(gr[0], 0, 0);
   issue(gr[1], min(1, max(ng - 1, 0)), 1);
+  if constexpr ((ABL & 128) != 0) tl[1] = ft_now();
 
   // ---- table: thread t writes entry t = {T(code[t >> 4]), T(code[t & 15])} into its 32 copies
   if (tid < 256) {
@@ -215,6 +254,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     if constexpr (NESTED) code2s[t] = c2v;
   }
   __syncthreads();
+  if constexpr ((ABL & 128) != 0) tl[2] = ft_now();
 
   const uint32_t lane4 = (uint32_t)(lane & 31) * 4;
   f32x4_t acc[RG][MT];
@@ -236,12 +276,33 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
         const int slot16 = (2 * bb + (g >> 1)) ^ ((rr >> 1) & 7);
         wv[rg] = *reinterpret_cast<const uint2*>(gs + rr * 128 + 16 * slot16 + 8 * (g & 1));
       }
+      // this block's token fragments (X8, odd block: rotated down from the lanes 8..15 of the pair's load)
+      uint4 xf[MT][2];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          if constexpr (X8 && (ABL & 1) == 0) {
+            if (bb & 1) {
+              const uint4 u = R.x[bb - 1][mt][s];
+              xf[mt][s] = make_uint4(__builtin_amdgcn_mov_dpp(u.x, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_mov_dpp(u.y, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_mov_dpp(u.z, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_mov_dpp(u.w, 0x128, 0xF, 0xF, false));
+            } else {
+              xf[mt][s] = R.x[bb][mt][s];
+            }
+          } else {
+            xf[mt][s] = R.x[bb][mt][s];
+          }
+        }
       f32x4_t blk[RG][MT];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
 #pragma unroll
         for (int rg = 0; rg < RG; ++rg) {
-          const uint32_t d = s ? wv[rg].y : wv[rg].x;
+          uint32_t d = s ? wv[rg].y : wv[rg].x;
+          if constexpr ((ABL & 64) != 0) d ^= R.wd[(rg * 2 + s + bb) % PIECES].x;
           uint32_t l[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {                      // byte i -> entry, lane copy -> bank
@@ -251,7 +312,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
           const uint4 bf = make_uint4(l[0], l[1], l[2], l[3]);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            blk[rg][mt] = FtMfma<T>::mma(R.x[bb][mt][s], bf, s ? blk[rg][mt] : f32x4_t{0.f, 0.f, 0.f, 0.f});
+            blk[rg][mt] = FtMfma<T>::mma(xf[mt][s], bf, s ? blk[rg][mt] : f32x4_t{0.f, 0.f, 0.f, 0.f});
         }
       }
 #pragma unroll
@@ -297,6 +358,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     consume(gr[0], gi + 2, 0);
   }
 
+  if constexpr ((ABL & 128) != 0) tl[6] = ft_now();
   // ---- the WAVES K shares meet in LDS, summed in wave order
   __syncthreads();                                          // every wave is done with the table and its ring
   float* red = reinterpret_cast<float*>(sm);
@@ -315,6 +377,11 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     for (int w = 1; w < WAVES; ++w) s += red[(w * NV * 4 + v) * 64 + lane];
     const int t = 16 * mt + 4 * g + i, col = r0 + 16 * rg + n;
     if (t < M && col < N) out[(long long)t * ldc + col] = Io<T>::from_f32(s);
+  }
+  if constexpr ((ABL & 128) != 0) {
+    tl[7] = ft_now();
+    if (lane == 0 && g_ft_tl != nullptr)
+      for (int i = 0; i < 8; ++i) g_ft_tl[((long long)blockIdx.x * WAVES + wave) * 8 + i] = tl[i];
   }
 }
 
@@ -367,31 +434,49 @@ bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uin
   auto go = [&](auto kern, int waves) {
     hipLaunchKernelGGL(kern, grid, dim3(64 * waves), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc);
   };
-  if (g_fewtok_mode >= 16) {                                // lab ablations: nested, <= 16 tokens, 48-row workgroups
-    if (!nested || n > 16 || rg != 3 || !s4) return false;
+  if (g_fewtok_mode >= 16) {                                // lab ablations: nested, <= 8 tokens, 48-row workgroups
+    if (!nested || n > 8 || rg != 3 || !s4) return false;
+    constexpr bool X8L = true;
     switch (g_fewtok_mode - 16) {
-      case 1: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 1>, 8); break;
-      case 2: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 2>, 8); break;
-      case 3: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 3>, 8); break;
-      case 4: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 4>, 8); break;
-      case 7: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 7>, 8); break;
-      case 32: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 32>, 8); break;
-      case 39: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, 39>, 8); break;
+      case 1: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 1>, 8); break;
+      case 2: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 2>, 8); break;
+      case 3: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 3>, 8); break;
+      case 4: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 4>, 8); break;
+      case 7: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 7>, 8); break;
+      case 32: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 32>, 8); break;
+      case 39: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 39>, 8); break;
+      case 64: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 64>, 8); break;
+      case 71: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 71>, 8); break;
+      case 128: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 128>, 8); break;
+      case 135: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 135>, 8); break;
       default: return false;
     }
     return true;
   }
+  const bool x8 = n <= 8;
   auto by_rg = [&](auto mt_tag, auto nested_tag, auto s4_tag) {
     constexpr int MT = decltype(mt_tag)::value;
     constexpr bool NS = decltype(nested_tag)::value, S = decltype(s4_tag)::value;
+    auto go_x8 = [&](auto rg_tag, auto waves_tag) {
+      constexpr int R = decltype(rg_tag)::value, W = decltype(waves_tag)::value;
+      if constexpr (MT == 1) {
+        if (x8) { go(k_gemm_4bit_fewtok<T, R, MT, NS, S, W, true>, W); return; }
+      }
+      go(k_gemm_4bit_fewtok<T, R, MT, NS, S, W, false>, W);
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
     switch (rg) {
-      case 1: go(k_gemm_4bit_fewtok<T, 1, MT, NS, S, 8>, 8); break;
-      case 2: go(k_gemm_4bit_fewtok<T, 2, MT, NS, S, 8>, 8); break;
+      case 1: go_x8(I1{}, I8{}); break;
+      case 2: go_x8(I2{}, I8{}); break;
       case 3:   // (17..32 tokens with per-block statistics: 4 waves, 8 would spill)
-        if constexpr (MT == 2 && !S) go(k_gemm_4bit_fewtok<T, 3, MT, NS, S, 4>, 4);
-        else go(k_gemm_4bit_fewtok<T, 3, MT, NS, S, 8>, 8);
+        if constexpr (MT == 2 && !S) go_x8(I3{}, I4{});
+        else go_x8(I3{}, I8{});
         break;
-      default: go(k_gemm_4bit_fewtok<T, 4, MT, NS, S, 4>, 4); break;
+      default: go_x8(I4{}, I4{}); break;
     }
   };
   auto by_s4 = [&](auto mt_tag, auto nested_tag) {
@@ -415,6 +500,10 @@ template bool launch_gemm_4bit_fewtok<fp16_t>(int, int, int, const fp16_t*, int,
 }  // namespace bnb
 
 extern "C" {
+// [lab, not in the header] timeline buffer of the ABL-128 variants (mode 16 + 128): 8 stamps per wave
+int cgemm_4bit_fewtok_timeline(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_ft_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
 // [additive, testing] whole-K few-token kernel: 0 = auto, 1 = off, 2 = wherever it fits
 void cgemm_4bit_set_fewtok_mode(int mode) { bnb::g_fewtok_mode = mode; }
 // [additive] 1 when the 4-bit GEMM entry points run the whole-K few-token kernel for out features m, n activation rows,
