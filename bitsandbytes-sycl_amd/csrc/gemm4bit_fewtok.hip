@@ -18,7 +18,7 @@
 //     so one 8-B operand read covers exactly one 64-element absmax block b and the block's two MFMAs sum unscaled
 //     T(code) x products; the absmax scale is one fma per accumulator after them -- no per-weight multiply or cast);
 //   * the table maps a packed byte straight to the MFMA operand dword {T(code[hi]), T(code[lo])} (32 bank-private
-//     copies, entry e of copy c at byte 128 e + 4 c: one bit-field extract + one shift-or per lookup);
+//     copies, entry e of copy c at byte 256 e + 4 c: one v_perm_b32 per lookup address);
 //   * tokens are the MFMA A operand (rows = tokens) read straight into registers through a buffer resource over rows
 //     0..M-1 (lanes of rows >= M get an out-of-range offset: zeros, no memory access, no branch).
 // The workgroup (4 waves) owns 16 RG weight rows and all of K; its waves take K in quarters of whole 4-block groups
@@ -50,7 +50,9 @@ __device__ __forceinline__ unsigned long long ft_now() {
 }
 
 constexpr int FT_THREADS = 256;
-constexpr int FT_TABLE = 256 * 128;     // 32 copies x 256 entries x 4 B
+// pair table: entry e of bank-private copy c at byte 256 e + 4 c (32 copies, 64 KiB span) so that a lookup address is
+// ONE v_perm_b32 of {packed dword, lane byte}; the nested code map sits in the entry rows' spare upper halves
+constexpr int FT_TABLE = 256 * 256;
 constexpr int FT_NG = 2;                // 4-block groups in flight per wave
 
 template <typename T> struct FtMfma;
@@ -67,7 +69,8 @@ template <> struct FtMfma<fp16_t> {
   }
 };
 
-template <int RG, int WAVES> constexpr int ft_lds_bytes() { return FT_TABLE + 1024 + WAVES * FT_NG * (16 * RG * 128); }
+template <int RG, int WAVES> constexpr int ft_lds_bytes() { return FT_TABLE + WAVES * FT_NG * (16 * RG * 128); }
+static_assert(ft_lds_bytes<3, 8>() <= 160 * 1024 && ft_lds_bytes<4, 4>() <= 160 * 1024, "LDS budget");
 
 // RG: 16-row weight groups per workgroup (and per wave); MT: 16-token A tiles (1: <= 16 tokens, 2: <= 32).
 // S4: blocksize 64 with K % 256 == 0 (and a nested group of >= 4 blocks): the four statistics of a row's group are
@@ -93,11 +96,11 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
   // VMEM instructions of one group, in issue order: tokens, statistics, then the DMA pieces
   static_assert(!X8 || MT == 1, "X8: one 16-token tile");
   constexpr int GROUP_OPS =
-      ((ABL & 1) ? 0 : (X8 ? 2 : 4) * MT * 2) + ((ABL & 2) ? 0 : (S4 ? 1 : 4) * RG * (NESTED ? 2 : 1)) + PIECES;
+      ((ABL & 1) ? 0 : (X8 ? 2 : 4) * MT * 2) + ((ABL & 2) ? 0 : (S4 ? 1 : 4 * RG) * (NESTED ? 2 : 1)) + PIECES;
   __shared__ __attribute__((aligned(16))) uint8_t sm[ft_lds_bytes<RG, WAVES>()];
   uint8_t* table = sm;
-  float* code2s = reinterpret_cast<float*>(sm + FT_TABLE);
-  uint8_t* ring = sm + FT_TABLE + 1024;
+  auto code2s_at = [&](uint32_t t) -> float& { return *reinterpret_cast<float*>(table + 256 * (t >> 5) + 128 + 4 * (t & 31)); };
+  uint8_t* ring = sm + FT_TABLE;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -138,6 +141,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
   long long sbase[RG];
 #pragma unroll
   for (int rg = 0; rg < RG; ++rg) sbase[rg] = 2LL * ldb * min(r0 + 16 * rg + n, N - 1);
+  const long long sbase_l = 2LL * ldb * min(r0 + 16 * min(g, RG - 1) + n, N - 1);   // S4: this lane's row group
   // DMA: piece j of a group = rows 8j .. 8j+7; lane l -> row 8j + (l >> 3), LDS slot l & 7 holding source slot
   // (l & 7) ^ ((row >> 1) & 7); slots past the row's end (the last, partial group) re-read its last slot (never used)
   const uint8_t* wsrc[PIECES];
@@ -156,9 +160,11 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     uint32_t q8[S4 ? 1 : 4][RG];
     float a2[S4 ? 1 : 4][RG];
     uint4 wd[(ABL & 64) ? PIECES : 1];                      // (lab ABL 64: the weight pieces in registers)
-    float4 am4[S4 ? RG : 1];                                // S4: the group's statistics as loaded (unpacked in use)
-    uint32_t q4[S4 ? RG : 1];
-    float a2g[S4 ? RG : 1];
+    // S4: the 4 statistics of row group min(g, RG - 1), row n -- one load per lane for ALL row groups of the wave
+    // (lanes g = 0 .. RG-1 each fetch one row group); consume() hands them to the other lanes by ds_bpermute
+    float4 am4;
+    uint32_t q4;
+    float a2g;
   };
   Group gr[FT_NG];
   auto issue = [&](Group& R, int gi, int slot) {            // this wave's group gi into ring slot `slot`
@@ -203,19 +209,15 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
       }
     }
     if constexpr ((ABL & 2) != 0 && S4) {
-#pragma unroll
-      for (int rg = 0; rg < RG; ++rg) { R.q4[rg] = 0x01010101u; R.a2g[rg] = 1.f; R.am4[rg] = make_float4(1.f, 1.f, 1.f, 1.f); }
+      R.q4 = 0x01010101u; R.a2g = 1.f; R.am4 = make_float4(1.f, 1.f, 1.f, 1.f);
     }
-    if constexpr ((ABL & 2) == 0 && S4) {                  // the group's 4 statistics per row in one load
-#pragma unroll
-      for (int rg = 0; rg < RG; ++rg) {
-        const long long j0 = (sbase[rg] >> 6) + 4LL * min(ga, ngr - 1);
-        if constexpr (NESTED) {
-          R.q4[rg] = *reinterpret_cast<const uint32_t*>(st.q8 + j0);
-          R.a2g[rg] = st.absmax2[j0 >> st.bs2_shift];
-        } else {
-          R.am4[rg] = *reinterpret_cast<const float4*>(st.absmax + j0);
-        }
+    if constexpr ((ABL & 2) == 0 && S4) {                  // the group's 4 statistics of row group min(g, RG-1)
+      const long long j0 = (sbase_l >> 6) + 4LL * min(ga, ngr - 1);
+      if constexpr (NESTED) {
+        R.q4 = *reinterpret_cast<const uint32_t*>(st.q8 + j0);
+        R.a2g = st.absmax2[j0 >> st.bs2_shift];
+      } else {
+        R.am4 = *reinterpret_cast<const float4*>(st.absmax + j0);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // this slot's previous ring reads are done (WAR)
@@ -250,8 +252,8 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     const int t = tid;
     const uint32_t v = Dot2<T>::pair(code_hi, code_lo);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 128 * t + 16 * ((k + t) & 7)) = make_uint4(v, v, v, v);
-    if constexpr (NESTED) code2s[t] = c2v;
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * t + 16 * ((k + t) & 7)) = make_uint4(v, v, v, v);
+    if constexpr (NESTED) code2s_at(t) = c2v;
   }
   __syncthreads();
   if constexpr ((ABL & 128) != 0) tl[2] = ft_now();
@@ -265,6 +267,25 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
 
   auto consume = [&](const Group& R, int gi, int slot) {
     const uint8_t* gs = my_ring + slot * GB;
+    // S4: row group rg's statistics come from lane 16 rg + n (ds_bpermute, one per dword)
+    uint32_t q4[S4 ? RG : 1];
+    float a2g[S4 ? RG : 1];
+    float4 am4[S4 ? RG : 1];
+    if constexpr (S4) {
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        const int src = 4 * (16 * rg + n);
+        if constexpr (NESTED) {
+          q4[rg] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)R.q4);
+          a2g[rg] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, R.a2g)));
+        } else {
+          am4[rg] = make_float4(__builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, R.am4.x))),
+                                __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, R.am4.y))),
+                                __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, R.am4.z))),
+                                __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, R.am4.w))));
+        }
+      }
+    }
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       if (4 * (g0 + gi) + bb >= nblk) break;                 // (wave-uniform) the partial last group
@@ -307,7 +328,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
 #pragma unroll
           for (int i = 0; i < 4; ++i) {                      // byte i -> entry, lane copy -> bank
             if constexpr ((ABL & 4) != 0) l[i] = d + i;
-            else l[i] = *reinterpret_cast<const uint32_t*>(table + ((__builtin_amdgcn_ubfe(d, 8 * i, 8) << 7) | lane4));
+            else l[i] = *reinterpret_cast<const uint32_t*>(table + __builtin_amdgcn_perm(d, lane4, 0x0C0C0000u | ((4u + i) << 8)));
           }
           const uint4 bf = make_uint4(l[0], l[1], l[2], l[3]);
 #pragma unroll
@@ -319,10 +340,10 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
       for (int rg = 0; rg < RG; ++rg) {
         float a;
         if constexpr (S4) {
-          if constexpr (NESTED) a = __fadd_rn(__fmul_rn(code2s[(R.q4[rg] >> (8 * bb)) & 0xFF], R.a2g[rg]), offset);
-          else a = bb == 0 ? R.am4[rg].x : bb == 1 ? R.am4[rg].y : bb == 2 ? R.am4[rg].z : R.am4[rg].w;
+          if constexpr (NESTED) a = __fadd_rn(__fmul_rn(code2s_at((q4[rg] >> (8 * bb)) & 0xFF), a2g[rg]), offset);
+          else a = bb == 0 ? am4[rg].x : bb == 1 ? am4[rg].y : bb == 2 ? am4[rg].z : am4[rg].w;
         } else {
-          if constexpr (NESTED) a = __fadd_rn(__fmul_rn(code2s[R.q8[bb][rg]], R.a2[bb][rg]), offset);
+          if constexpr (NESTED) a = __fadd_rn(__fmul_rn(code2s_at(R.q8[bb][rg]), R.a2[bb][rg]), offset);
           else a = R.am[bb][rg];
         }
 #pragma unroll
