@@ -451,6 +451,25 @@ def bench_llama2_70b_shard(dev, ranks=8, prefill_tokens=4096, layer_copies=8, it
     wbytes = sum(n * k // 2 + n * k // BS + n * k // BS // 256 * 4 + 1024 for n, k in shapes)
     res["decode"] = {"layer_us": t_layer * 1e6, "weight_bytes_per_layer": wbytes, "gbs": wbytes / t_layer / 1e9,
                      "frac_of_hbm": wbytes / t_layer / 1e9 / PEAK_HBM_GBS, "model_80_layers_ms": 80 * t_layer * 1e3}
+    # the same layers with the projections that share an input fused (parallel.fuse_quantized_4bit): q/k/v one
+    # 1280 x 8192 weight, gate/up one 7168 x 8192 -- four launches per layer instead of seven
+    from python_src_quants.parallel import fuse_quantized_4bit
+    fused = []
+    for ws in layers:
+        qkv = fuse_quantized_4bit([ws[0], ws[1], ws[2]])[:2]
+        gu = fuse_quantized_4bit([ws[4], ws[5]])[:2]
+        fused.append([qkv, ws[3], gu, ws[6]])
+    fshapes = [(shapes[0][0] + shapes[1][0] + shapes[2][0], hid), shapes[3], (2 * shapes[4][0], hid), shapes[6]]
+    fout = {i: torch.empty(1, n, device=dev, dtype=torch.bfloat16) for i, (n, _) in enumerate(fshapes)}
+    fcalls = [(lambda q=q, st=st, i=i, k=k: F.gemv_4bit(x if k == hid else xi, q.t(), out=fout[i], state=st))
+              for ws in fused for i, ((n, k), (q, st)) in enumerate(zip(fshapes, ws))]
+    tf = _time_graph(fcalls, 10) * len(fshapes)
+    fbytes = sum(n * k // 2 + n * k // BS + n * k // BS // 256 * 4 + 1024 for n, k in fshapes)
+    res["decode_fused"] = {"layer_us": tf * 1e6, "launches_per_layer": len(fshapes), "weight_bytes_per_layer": fbytes,
+                           "gbs": fbytes / tf / 1e9, "frac_of_hbm": fbytes / tf / 1e9 / PEAK_HBM_GBS,
+                           "model_80_layers_ms": 80 * tf * 1e3,
+                           "fused": "q/k/v -> 1280 x 8192, gate/up -> 7168 x 8192 (parallel.fuse_quantized_4bit)"}
+    del fused, fcalls
     res["note"] = ("rank-local compute only (no all-gather); decode over 8 distinct layers (~430 MB) from one HIP "
                    "graph; prefill path per shape from the measured route")
     del layers, calls

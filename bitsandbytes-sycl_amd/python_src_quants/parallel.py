@@ -77,6 +77,52 @@ def shard_quantized_4bit(packed: torch.Tensor, state: "F.QuantState", world: int
                            dtype=state.dtype, offset=offset, state2=state2)
 
 
+def fuse_quantized_4bit(parts):
+    """Concatenate already quantised 4-bit weights [n_i, K] along the output features into ONE weight
+    [sum n_i, K] -- the inverse of shard_quantized_4bit, for projections that read the same input (a decoder
+    layer's q/k/v, or gate/up): one GEMV / GEMM launch then streams all of them (round 3, bench
+    `llama2_70b_rank_shard_config5.decode_fused`).  `parts` is a list of (packed, QuantState) with equal K,
+    blocksize, quant_type, code and dtype.  Returns (packed [(N*K)//2, 1] uint8, QuantState with shape (N, K)) and the
+    output column offsets [0, n_0, n_0 + n_1, ...] (split the result with split_fused_columns).
+
+    Packed bytes and first-level statistics concatenate exactly (K % blocksize == 0: no block straddles two rows).
+    Compressed (nested) statistics are decoded and re-compressed for the fused weight (offset = their mean, dynamic
+    8-bit map, the nested blocksize) -- what quantize_4bit stores for the concatenated rows; each part's offset is
+    its own mean, so the codes of the parts alone cannot simply be concatenated."""
+    if not parts:
+        raise ValueError("fuse_quantized_4bit: no parts")
+    K = parts[0][1].shape[1]
+    st0 = parts[0][1]
+    for _, st in parts:
+        if (st.shape[1] != K or st.blocksize != st0.blocksize or st.quant_type != st0.quant_type
+                or st.dtype != st0.dtype or bool(st.nested) != bool(st0.nested)
+                or not torch.equal(st.code, st0.code)):
+            raise ValueError("fuse_quantized_4bit: parts need equal K, blocksize, quant_type, code, dtype and "
+                             "statistics format")
+    if K % st0.blocksize or K % 2:
+        raise ValueError("fuse_quantized_4bit needs K % blocksize == 0 and even K")
+    packed = torch.cat([p.reshape(-1) for p, _ in parts]).reshape(-1, 1)
+    N = sum(st.shape[0] for _, st in parts)
+    offsets = [0]
+    for _, st in parts:
+        offsets.append(offsets[-1] + st.shape[0])
+    shape = torch.Size([N, K])
+    if not st0.nested:
+        absmax = torch.cat([st.absmax for _, st in parts])
+        return packed, F.QuantState(absmax=absmax, shape=shape, code=st0.code, blocksize=st0.blocksize,
+                                    quant_type=st0.quant_type, dtype=st0.dtype), offsets
+    absmax = torch.cat([F._absmax_fp32(st) for _, st in parts]).contiguous()
+    offset = absmax.mean()
+    qabsmax, state2 = F.quantize_blockwise(absmax - offset, blocksize=st0.state2.blocksize)
+    return packed, F.QuantState(absmax=qabsmax, shape=shape, code=st0.code, blocksize=st0.blocksize,
+                                quant_type=st0.quant_type, dtype=st0.dtype, offset=offset, state2=state2), offsets
+
+
+def split_fused_columns(y: torch.Tensor, offsets):
+    """Views of the fused output's column ranges (fuse_quantized_4bit offsets), one per original projection."""
+    return [y[..., a:b] for a, b in zip(offsets[:-1], offsets[1:])]
+
+
 def shard_int8_rows(CB: torch.Tensor, SCB: torch.Tensor, world: int, rank: int):
     """Rank `rank`'s output-feature shard of an LLM.int8 weight: the rows of CB (int8 [N, K], row-normalised) and
     of its row statistics SCB (fp32 [N]) -- Int8Params' state (ref:nn/modules.py:559-632).  Rows quantise

@@ -195,3 +195,45 @@ def test_metric_shape_bits_reproducible_across_processes(dev):
         assert r.returncode == 0, r.stderr[-2000:]
         digests.append([ln for ln in r.stdout.splitlines() if ln.startswith("DIGEST")][0])
     assert digests[0] == digests[1]
+
+
+@pytest.mark.parametrize("nested", [False, True])
+def test_fused_projections_70b_shard(dev, nested):
+    """Config 5 decode with the projections that share an input fused (parallel.fuse_quantized_4bit): one rank's
+    q/k/v (1024 + 128 + 128 rows) and gate/up (2 x 3584 rows) x 8192.  Packed bytes (and plain statistics)
+    concatenate exactly; nested statistics are re-compressed for the fused weight and decode within the nested code's
+    resolution of the parts'.  The fused GEMV and few-token GEMM agree with the fp64 oracle on the fused state, and
+    each column range with the part's own GEMV within the GEMV tolerance."""
+    F = _F()
+    from python_src_quants.parallel import fuse_quantized_4bit, split_fused_columns
+    torch.manual_seed(11 + nested)
+    K = 8192
+    for rows in ((1024, 128, 128), (3584, 3584)):
+        parts = []
+        for n in rows:
+            W = (torch.randn(n, K, device=dev) * 0.02).to(torch.bfloat16)
+            parts.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested))
+            del W
+        q, st, offs = fuse_quantized_4bit(parts)
+        N = sum(rows)
+        assert st.shape == (N, K) and offs == [0] + list(np.cumsum(rows))
+        assert torch.equal(q.reshape(-1), torch.cat([p.reshape(-1) for p, _ in parts]))
+        am_f = F._absmax_fp32(st)
+        am_p = torch.cat([F._absmax_fp32(s) for _, s in parts])
+        if nested:
+            assert (am_f - am_p).abs().max().item() <= 0.02 * am_p.abs().max().item()
+        else:
+            assert torch.equal(am_f, am_p)
+        for M in (1, 8):
+            X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            Y = F.gemv_4bit(X, q.t(), state=st) if M == 1 else F.gemm_4bit(X, q, st)
+            Y = Y.reshape(M, N)
+            exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), am_f.cpu().numpy(), N, K, 64,
+                                            st.code.cpu().numpy(), "bf16")
+            rms = np.sqrt(np.mean(exp ** 2))
+            err = np.abs(Y.float().cpu().numpy().astype(np.float64) - exp)
+            assert np.all(err <= 2e-2 * rms + 2e-2 * np.abs(exp)), float(err.max())
+            for (pq, pst), y in zip(parts, split_fused_columns(Y, offs)):
+                yp = (F.gemv_4bit(X, pq.t(), state=pst) if M == 1 else F.gemm_4bit(X, pq, pst)).reshape(M, -1).float()
+                r = yp.pow(2).mean().sqrt().item()
+                assert (y.float() - yp).abs().max().item() <= 4e-2 * r + 4e-2 * yp.abs().max().item()
