@@ -366,6 +366,16 @@ bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uin
   return true;
 }
 
+// out[t, n] = T(sum_s ws[s][t][n]) for any producer of row-major fp32 split partials (the split-K of k_hgemm too)
+template <typename T>
+void launch_splitk_rows_reduce(const float* ws, int nsplit, int rows, int cols, T* out, int ldc) {
+  const long long mn = (long long)rows * cols;
+  hipLaunchKernelGGL((k_skinny_reduce<T>), dim3((unsigned)((mn / 4 + 255) / 256 + 1)), dim3(256), 0, current_stream(), ws,
+                     nsplit, rows, cols, out, ldc);
+}
+template void launch_splitk_rows_reduce<bf16_t>(const float*, int, int, int, bf16_t*, int);
+template void launch_splitk_rows_reduce<fp16_t>(const float*, int, int, int, fp16_t*, int);
+
 template bool launch_gemm_4bit_skinny<bf16_t>(int, int, int, const bf16_t*, int, const uint8_t*, int, SkStats, int, int,
                                               const float*, bf16_t*, int, float*, long long);
 template bool launch_gemm_4bit_skinny<fp16_t>(int, int, int, const fp16_t*, int, const uint8_t*, int, SkStats, int, int,

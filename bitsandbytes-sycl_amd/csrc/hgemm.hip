@@ -22,6 +22,7 @@
 #include "gemm_common.hpp"
 #include "int8_common.hpp"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace bnb {
@@ -144,23 +145,33 @@ __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r
 //   copies, 2048 = no fragment re-reads (profiles/lab/r03_hgemm_ablation.txt).  Launched: 8 + 16 + 4096.
 constexpr int HG_V = 8 + 16 + 4096;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
-template <int OP, int V = 0>
+// SPLIT (bf16 / fp16 only): the split-K form -- its epilogue stores fp32 partials only.  A separate instantiation, so
+// that each kernel has ONE epilogue reading the accumulators (two in one kernel made the allocator spill).
+template <int OP, int V = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(HG_THREADS, 1)
 k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const void* __restrict__ Bv, long long ldb,
         void* __restrict__ Cv, long long ldc, const float* __restrict__ rowStats, const float* __restrict__ colStats,
-        const fp16_t* __restrict__ bias) {
+        const fp16_t* __restrict__ bias, float* __restrict__ ws, int ksplit, int kchunk) {
   using Op = HgOpT<OP>;
   using acc_t = typename Op::acc_t;
   constexpr int E = Op::ELEM;
-  const uint8_t* A = reinterpret_cast<const uint8_t*>(Av);
-  const uint8_t* B = reinterpret_cast<const uint8_t*>(Bv);
+  // split-K (ksplit > 1, small tile grids): workgroup = (tile, split s); split s multiplies k-tiles
+  // [s * kchunk, min((s + 1) * kchunk, all)) and stores fp32 partials ws[s][M][N] (summed in split order afterwards)
+  const int tiles_all = ((N + HG_BN - 1) / HG_BN) * ((M + HG_BM - 1) / HG_BM);
+  // (readfirstlane: the divisions by the runtime ksplit run on the VALU; their wave-uniform results must live in SGPRs,
+  // not in two of the main loop's 256 VGPRs -- that spilled)
+  const int wgs = xcd_remap(blockIdx.x, tiles_all * (SPLIT ? ksplit : 1));
+  const int split = SPLIT ? __builtin_amdgcn_readfirstlane(wgs % ksplit) : 0;
+  const int kt0 = split * kchunk;
+  const uint8_t* A = reinterpret_cast<const uint8_t*>(Av) + (long long)kt0 * 128;
+  const uint8_t* B = reinterpret_cast<const uint8_t*>(Bv) + (long long)kt0 * 128;
   __shared__ __attribute__((aligned(16))) uint8_t smem[HG_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // ---- tile order: XCD-contiguous ids; groups of 4 M-tiles x all N-tiles (an XCD's 32 tiles share A / B rows)
   const int tilesN = (N + HG_BN - 1) / HG_BN, tilesM = (M + HG_BM - 1) / HG_BM;
-  const int wg = xcd_remap(blockIdx.x, tilesN * tilesM);
+  const int wg = SPLIT ? __builtin_amdgcn_readfirstlane(wgs / ksplit) : wgs;
   constexpr int GROUP = 4;
   const int group_span = GROUP * tilesN;
   const int first_m = (wg / group_span) * GROUP;
@@ -206,7 +217,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
 
   acc_t acc[8][8];
   frag_t w0[8], x0[8], w1[8], x1[8];
-  const int nk = K * E / 128;                   // k-tiles of 128 bytes
+  const int nk = min(kchunk, K * E / 128 - kt0);   // k-tiles of 128 bytes in this split (>= 1 by the host rule)
 
   // V & 512 (lab): register-staged copies instead of LDS-DMA -- ordinary 16-B global loads into 16 staging registers
   // (same swizzled source offsets), written to the same LDS slots one k-tile later by ds_write_b128.  The writes of
@@ -392,7 +403,31 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   auto value = [&](int j, int i, int r, int n, float rs) -> float {   // HG_I8_DEQ: mm_dequant of one element
     return (float)Io<fp16_t>::to_f32(mm_dequant_value(acc[j][i][r], rs, colStats[n], bias ? (float)bias[n] : 0.0f));
   };
-  if (full && OUT == 2) {
+  if constexpr (SPLIT) {
+    // fp32 partials of this split: acc[j][i] = C[mb + 16 i][nb + 16 j .. +3], one 16-B store each (N % 4 == 0 on the
+    // host rule), rows / columns past the edge skipped
+    // Buffer stores (SGPR base, one 32-bit lane offset) of the accumulator AGPRs themselves: a 64-bit address and 4
+    // data VGPRs per store need registers the main loop does not leave (the int32 form of this epilogue spilled, and
+    // the builtin 8-B store form miscompiled to copies of element 0); edge elements go out of range (offset past
+    // num_records: the store is dropped).  After the MFMA -> read pad above, like every other accumulator read.
+    if constexpr (OP == HG_BF16 || OP == HG_FP16) {
+      const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(ws + (long long)split * M * N, (short)0,
+                                                                          (int)((long long)M * N * 4), 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = mb + 16 * i;
+        const uint32_t rowoff = (uint32_t)m * (uint32_t)N * 4u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = nb + 16 * j;
+          const uint32_t off = (m < M && n < N) ? rowoff + 4u * (uint32_t)n : 0x80000000u;
+          // straight from the accumulator AGPRs (stores take AGPR data on gfx950): no VGPRs, no reads to schedule
+          asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" : : "a"(acc[j][i]), "v"(off), "s"(wr) : "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  } else if (full && OUT == 2) {
     // 16-bit outputs of a full tile: staged through LDS so every global store writes whole 256-B row segments
     // (direct 8-B fragment stores put 16 rows x 32 B in one instruction: +4 us of epilogue per launch at 4096^2)
     __syncthreads();                                   // every wave is past its last stage read
@@ -482,12 +517,52 @@ bool hgemm_fits(int m, int n, int k, long long lda, long long ldb, const void* A
 
 long long hgemm_tiles(int m, int n) { return (long long)((m + HG_BM - 1) / HG_BM) * ((n + HG_BN - 1) / HG_BN); }
 
+// Split-K for tile grids below HG_SPLIT_TILES (the 8-way-shard and mid-size prefill shapes: 4096 x 1024 is 64 tiles
+// on 256 CUs): S = the splits that bring the grid to about one workgroup per CU, each split >= HG_SPLIT_MIN_KT
+// k-tiles, at most 8; fp32 partials ws[S][m][n] summed in split order by one reduce launch (deterministic).
+constexpr int HG_SPLIT_TILES = 192, HG_SPLIT_MIN_KT = 8, HG_SPLIT_MAX = 8;
+struct HgSplit {
+  int splits, kchunk;
+};
+HgSplit hgemm_split(int m, int n, int k, int elem) {
+  const long long tiles = hgemm_tiles(m, n);
+  const int nkt = (int)((long long)k * elem / 128);
+  if (tiles >= HG_SPLIT_TILES || n % 4) return HgSplit{1, nkt};
+  int s = (int)std::min<long long>(HG_SPLIT_MAX, (256 + tiles - 1) / tiles);
+  s = std::max(1, std::min(s, nkt / HG_SPLIT_MIN_KT));
+  const int kchunk = (nkt + s - 1) / s;
+  return HgSplit{(nkt + kchunk - 1) / kchunk, kchunk};
+}
+long long hgemm_workspace_bytes(int m, int n, int k, int elem) {
+  const HgSplit sp = hgemm_split(m, n, k, elem);
+  return sp.splits > 1 ? (long long)sp.splits * m * n * (long long)sizeof(float) : 0;
+}
+
 template <int OP>
 int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* B, long long ldb, void* C, long long ldc,
-                 const float* rowStats = nullptr, const float* colStats = nullptr, const fp16_t* bias = nullptr) {
+                 const float* rowStats = nullptr, const float* colStats = nullptr, const fp16_t* bias = nullptr,
+                 float* ws = nullptr, long long ws_bytes = 0) {
   if (!hgemm_fits(m, n, k, lda, ldb, A, B, HgOpT<OP>::ELEM) || ldc < n) return 1;
-  hipLaunchKernelGGL((k_hgemm<OP, HG_V>), dim3((unsigned)hgemm_tiles(m, n)), dim3(HG_THREADS), 0, current_stream(), m,
-                     n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias);
+  HgSplit sp{1, (int)((long long)k * HgOpT<OP>::ELEM / 128)};
+  if constexpr (OP == HG_BF16 || OP == HG_FP16) {
+    const HgSplit want = hgemm_split(m, n, k, HgOpT<OP>::ELEM);
+    if (want.splits > 1 && ws != nullptr && ((uintptr_t)ws & 15) == 0 &&
+        ws_bytes >= (long long)want.splits * m * n * (long long)sizeof(float))
+      sp = want;
+  }
+  if (sp.splits > 1) {
+    if constexpr (OP == HG_BF16 || OP == HG_FP16)
+      hipLaunchKernelGGL((k_hgemm<OP, HG_V, true>), dim3((unsigned)(hgemm_tiles(m, n) * sp.splits)), dim3(HG_THREADS), 0,
+                         current_stream(), m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sp.splits,
+                         sp.kchunk);
+  } else {
+    hipLaunchKernelGGL((k_hgemm<OP, HG_V>), dim3((unsigned)hgemm_tiles(m, n)), dim3(HG_THREADS), 0, current_stream(), m,
+                       n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, sp.kchunk);
+  }
+  if constexpr (OP == HG_BF16 || OP == HG_FP16) {
+    using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
+    if (sp.splits > 1) launch_splitk_rows_reduce<T>(ws, sp.splits, m, n, reinterpret_cast<T*>(C), (int)ldc);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error((int)e, "k_hgemm launch");
@@ -521,5 +596,17 @@ int chgemm_tn_bf16(int m, int n, int k, const bf16_t* A, int lda, const bf16_t* 
 int chgemm_tn_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* W, int ldw, fp16_t* C, int ldc) {
   return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc);
 }
+// [additive] the same with a caller workspace for split-K on small tile grids (< 192 tiles of 256 x 256: fp32
+// partials, summed in split order by one more launch; same bits on every call).  chgemm_tn_workspace_bytes gives the
+// bytes the shape needs (0: no split); a smaller workspace runs the unsplit kernel.
+int chgemm_tn_ws_bf16(int m, int n, int k, const bf16_t* A, int lda, const bf16_t* W, int ldw, bf16_t* C, int ldc,
+                      float* ws, long long ws_bytes) {
+  return bnb::hgemm_launch<bnb::HG_BF16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
+}
+int chgemm_tn_ws_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* W, int ldw, fp16_t* C, int ldc,
+                      float* ws, long long ws_bytes) {
+  return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
+}
+long long chgemm_tn_workspace_bytes(int m, int n, int k) { return bnb::hgemm_workspace_bytes(m, n, k, 2); }
 
 }  // extern "C"

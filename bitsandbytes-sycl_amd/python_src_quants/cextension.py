@@ -37,6 +37,7 @@ class BNBNativeLibrary:
         lib.cget_last_error_message.restype = ct.c_char_p
         lib.cgemm_4bit_workspace_bytes.restype = ct.c_longlong
         lib.cigemmlt_workspace_bytes.restype = ct.c_longlong
+        lib.chgemm_tn_workspace_bytes.restype = ct.c_longlong
         for name in ("cigemmlt_turing_32", "cigemmlt_turing_8", "cigemmlt_turing_8_rowscale",
                      "cigemmlt_ampere_32", "cigemmlt_ampere_8", "cigemmlt_ampere_8_rowscale",
                      "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cigemmlt_row_dequant_ws_fp16",
@@ -47,7 +48,7 @@ class BNBNativeLibrary:
                      "cdequantize_blockwise_nested_fp16_fp4", "cdequantize_blockwise_nested_fp16_nf4",
                      "cdequantize_blockwise_nested_bf16_fp4", "cdequantize_blockwise_nested_bf16_nf4",
                      "cint8_row_quant_fp16", "cgemm_4bit_inference_nested_ws_bf16",
-                     "cgemm_4bit_inference_nested_ws_fp16", "cset_cpu_threads", "cgemm_4bit_fewtok_takes"):
+                     "cgemm_4bit_inference_nested_ws_fp16", "cset_cpu_threads", "cgemm_4bit_fewtok_takes", "chgemm_tn_ws_bf16", "chgemm_tn_ws_fp16"):
             getattr(lib, name).restype = ct.c_int
 
     def __getattr__(self, item):

@@ -839,11 +839,18 @@ def gemm_4bit_measured_route(A: Tensor, state: QuantState, absmax: Optional[Tens
     return _ROUTES.get(_route_key(A.reshape(-1, state.shape[1]), state, absmax))
 
 
+HGEMM_SPLIT_MIN_K = 16384
+
+
 def _hgemm_fits(rows: int, N: int, K: int) -> bool:
-    """chgemm_tn's own rule (k % 64, 32-bit lane offsets) plus a tile grid that fills the chip."""
+    """chgemm_tn's own rule (k % 64, 32-bit lane offsets) plus where it is the static choice: a tile grid that fills
+    the chip, or a long K on a smaller grid (split-K over the GEMM workspace, chgemm_tn_ws_*).  Measured
+    (tools/route_probe3.py, profiles/lab/r03_routes.txt): 4096 x 1024 x 28672 (the 70B down-projection shard) 207 us
+    split-K against 342 (torch.matmul) and 228 (rocBLAS searched); below K = 16384 the small grids stay on
+    torch.matmul (4096 x 1024 x 8192 74.8 vs 76.7 us, 2048 x 3584 x 8192 114.7 vs 152.9)."""
     tiles = ((rows + 255) // 256) * ((N + 255) // 256)
-    return (K % 64 == 0 and tiles >= HGEMM_MIN_TILES and (rows - 1) * K * 2 + 2 * K <= 0xFFFFFFFF
-            and (N - 1) * K * 2 + 2 * K <= 0xFFFFFFFF)
+    return (K % 64 == 0 and (tiles >= HGEMM_MIN_TILES or (K >= HGEMM_SPLIT_MIN_K and N % 4 == 0))
+            and (rows - 1) * K * 2 + 2 * K <= 0xFFFFFFFF and (N - 1) * K * 2 + 2 * K <= 0xFFFFFFFF)
 
 
 def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
@@ -1055,10 +1062,12 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         elif ev:
             ev[1].record()
         if route == "hgemm":
-            # the hand-written GEMM (hgemm.hip)
-            fn = lib.chgemm_tn_bf16 if A.dtype == torch.bfloat16 else lib.chgemm_tn_fp16
+            # the hand-written GEMM (hgemm.hip); split-K over a workspace on small tile grids (chgemm_tn_ws_*)
+            ws_bytes = int(lib.chgemm_tn_workspace_bytes(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K)))
+            ws = _gemm_workspace(A.device, ws_bytes)
+            fn = lib.chgemm_tn_ws_bf16 if A.dtype == torch.bfloat16 else lib.chgemm_tn_ws_fp16
             rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W),
-                    ct.c_int32(K), get_ptr(out), ct.c_int32(N))
+                    ct.c_int32(K), get_ptr(out), ct.c_int32(N), get_ptr(ws), ct.c_longlong(ws_bytes))
             post_call(prev_device)
             if rc:
                 raise RuntimeError(f"bitsandbytes HIP GEMM (chgemm_tn) returned {rc}: "

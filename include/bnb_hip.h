@@ -218,6 +218,14 @@ int cgemm_tn_plan(int m, int n, int k, int dtype, int lda, int ldw, int ldc);
  * 16-B aligned; nothing launched), 2 = launch error (cget_last_error*). */
 int chgemm_tn_bf16(int m, int n, int k, const bnb_bf16* A, int lda, const bnb_bf16* W, int ldw, bnb_bf16* C, int ldc);
 int chgemm_tn_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp16* W, int ldw, bnb_fp16* C, int ldc);
+/* [additive] the same with a caller workspace: split-K (fp32 partials, summed in split order by one more launch) on
+ * tile grids below 192 tiles of 256 x 256; chgemm_tn_workspace_bytes(m, n, k) gives the bytes the shape needs (0 = no
+ * split); a smaller workspace runs the unsplit kernel.  Same return codes. */
+int chgemm_tn_ws_bf16(int m, int n, int k, const bnb_bf16* A, int lda, const bnb_bf16* W, int ldw, bnb_bf16* C, int ldc,
+                      float* ws, long long ws_bytes);
+int chgemm_tn_ws_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp16* W, int ldw, bnb_fp16* C, int ldc,
+                      float* ws, long long ws_bytes);
+long long chgemm_tn_workspace_bytes(int m, int n, int k);
 /* [additive, measurement] measured ceilings for the bench's roofline (probe.hip): the dense MFMA rate on random operands
  * in registers (kind 0 = bf16 v_mfma_f32_16x16x32_bf16, 1 = int8 v_mfma_i32_16x16x64_i8; one wave per SIMD, 8 x iters
  * MFMAs per wave; sink >= blocks * 256 floats) and the HBM streaming read rate (bytes % 16 == 0; sink >= blocks

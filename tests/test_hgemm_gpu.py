@@ -34,6 +34,20 @@ def _hgemm(F, X, W, out=None, lda=None, ldw=None):
     return rc, out
 
 
+def _hgemm_ws(F, X, W):
+    """chgemm_tn_ws_* with the workspace its rule asks for (split-K on small tile grids), as gemm_4bit calls it."""
+    m, k = X.shape
+    n = W.shape[0]
+    out = torch.empty(m, n, device=X.device, dtype=X.dtype)
+    nbytes = int(F.lib.chgemm_tn_workspace_bytes(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k)))
+    ws = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=X.device)
+    fn = F.lib.chgemm_tn_ws_bf16 if X.dtype == torch.bfloat16 else F.lib.chgemm_tn_ws_fp16
+    F.pre_call(X.device)
+    rc = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(X), ct.c_int32(k), F.get_ptr(W), ct.c_int32(k),
+            F.get_ptr(out), ct.c_int32(n), F.get_ptr(ws), ct.c_longlong(nbytes))
+    return rc, out
+
+
 def _check(Y, X, W):
     exp = torch.matmul(X.float(), W.float().t())
     rel = 2.0 ** -8 if Y.dtype == torch.bfloat16 else 2.0 ** -11
@@ -123,7 +137,7 @@ def test_gemm_4bit_hgemm_route_vs_oracle(dev, dtype, nested):
     X = torch.randn(M, K, device=dev, dtype=dtype)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
     Y = F.gemm_4bit(X, q, st, _route="hgemm")
-    _, Yd = _hgemm(F, X, F.dequantize_4bit(q, st))
+    _, Yd = _hgemm_ws(F, X, F.dequantize_4bit(q, st))     # (24 tiles: the route runs split-K)
     assert torch.equal(Y, Yd)
     absmax = F._absmax_fp32(st).cpu().numpy()
     exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64, st.code.cpu().numpy(),
@@ -159,3 +173,37 @@ def test_int8_on_the_4wave_kernel_is_bit_identical(dev, mnk):
     assert torch.equal(outs[4][0], outs[0][0])
     exact = (A.double() @ B.double().t())
     assert torch.equal(outs[4][1].double(), exact)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mnk", [(4096, 1024, 8192), (4096, 1024, 28672), (1000, 1100, 4096), (512, 11008, 4096),
+                                 (257, 516, 1024), (2048, 3584, 8192), (300, 260, 576)])
+def test_hgemm_split_k_against_fp32_product(dev, dtype, mnk):
+    """Small tile grids (< 192 tiles) through chgemm_tn_ws_*: split-K over fp32 partials in the caller's workspace,
+    summed in split order -- within the same fp32-product bound as the unsplit kernel (the k order differs, the
+    accumulation is fp32 either way), deterministic across calls, and the workspace query matches the split
+    (0 when the shape is not split); a too-small workspace runs the unsplit kernel."""
+    F = _F()
+    m, n, k = mnk
+    g = torch.Generator(device=dev).manual_seed(m + n + k)
+    X = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    W = (torch.rand(n, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    nbytes = int(F.lib.chgemm_tn_workspace_bytes(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k)))
+    tiles = ((m + 255) // 256) * ((n + 255) // 256)
+    assert (nbytes > 0) == (tiles < 192 and n % 4 == 0 and k >= 2 * 8 * 64)
+    ws = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=dev)
+    fn = F.lib.chgemm_tn_ws_bf16 if dtype == torch.bfloat16 else F.lib.chgemm_tn_ws_fp16
+    outs = []
+    for wsb in (nbytes, nbytes, 0):
+        out = torch.empty(m, n, device=dev, dtype=dtype)
+        F.pre_call(dev)
+        rc = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(X), ct.c_int32(k), F.get_ptr(W), ct.c_int32(k),
+                F.get_ptr(out), ct.c_int32(n), F.get_ptr(ws), ct.c_longlong(wsb))
+        torch.cuda.synchronize()
+        assert rc == 0
+        _check(out, X, W)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    rc, Yu = _hgemm(F, X, W)                        # the plain entry point runs the unsplit kernel
+    torch.cuda.synchronize()
+    assert torch.equal(Yu, outs[2])
