@@ -110,6 +110,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
   const int g0 = wave * ngr / WAVES, ng = (wave + 1) * ngr / WAVES - g0;   // this wave's groups (may be 0)
   const int rowbytes = K >> 1;
   unsigned long long tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlw0 = 0, tlw1 = 0, tlw2 = 0;   // group 0 / 1 / 2 landed
   if constexpr ((ABL & 128) != 0) tl[0] = ft_now();
 
   // ---- table values first (the VMEM counter retires in order)
@@ -236,7 +237,11 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
     if (next_issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GROUP_OPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr ((ABL & 128) != 0) {
-      if (nwait < 3) tl[3 + nwait] = ft_now();
+      // constant indices only: a dynamic one puts tl[] in scratch, and scratch waves launch late (skews the stamps)
+      const unsigned long long now = ft_now();
+      tlw0 = nwait == 0 ? now : tlw0;
+      tlw1 = nwait == 1 ? now : tlw1;
+      tlw2 = nwait == 2 ? now : tlw2;
       ++nwait;
     }
   };
@@ -286,16 +291,32 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
         }
       }
     }
+    // this lane's 8 packed bytes of block bb: row 16 rg + n, bytes 32 bb + 8 g .. +7 = 16-B slot 2 bb + (g >> 1);
+    // all four blocks' reads up front (S4: the group is always whole, so one basic block and no LDS drain per block)
+    uint2 wvg[4][RG];
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      if (4 * (g0 + gi) + bb >= nblk) break;                 // (wave-uniform) the partial last group
-      // this lane's 8 packed bytes of block bb: row 16 rg + n, bytes 32 bb + 8 g .. +7 = 16-B slot 2 bb + (g >> 1)
-      uint2 wv[RG];
+    for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
       for (int rg = 0; rg < RG; ++rg) {
         const int rr = 16 * rg + n;
         const int slot16 = (2 * bb + (g >> 1)) ^ ((rr >> 1) & 7);
-        wv[rg] = *reinterpret_cast<const uint2*>(gs + rr * 128 + 16 * slot16 + 8 * (g & 1));
+        if (S4 || bb == 0) wvg[bb][rg] = *reinterpret_cast<const uint2*>(gs + rr * 128 + 16 * slot16 + 8 * (g & 1));
+      }
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      if (!S4 && 4 * (g0 + gi) + bb >= nblk) break;          // (wave-uniform) the partial last group
+      uint2 wv[RG];
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        if constexpr (S4) {
+          wv[rg] = wvg[bb][rg];
+        } else if (bb == 0) {
+          wv[rg] = wvg[0][rg];
+        } else {
+          const int rr = 16 * rg + n;
+          const int slot16 = (2 * bb + (g >> 1)) ^ ((rr >> 1) & 7);
+          wv[rg] = *reinterpret_cast<const uint2*>(gs + rr * 128 + 16 * slot16 + 8 * (g & 1));
+        }
       }
       // this block's token fragments (X8, odd block: rotated down from the lanes 8..15 of the pair's load)
       uint4 xf[MT][2];
@@ -401,7 +422,11 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
   }
   if constexpr ((ABL & 128) != 0) {
     tl[7] = ft_now();
+    tl[3] = tlw0;
+    tl[4] = tlw1;
+    tl[5] = tlw2;
     if (lane == 0 && g_ft_tl != nullptr)
+#pragma unroll
       for (int i = 0; i < 8; ++i) g_ft_tl[((long long)blockIdx.x * WAVES + wave) * 8 + i] = tl[i];
   }
 }
@@ -456,8 +481,14 @@ bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uin
     hipLaunchKernelGGL(kern, grid, dim3(64 * waves), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc);
   };
   if (g_fewtok_mode >= 16) {                                // lab ablations: nested, <= 8 tokens, 48-row workgroups
-    if (!nested || n > 8 || rg != 3 || !s4) return false;
+    if (!nested || n > 8 || !s4) return false;
     constexpr bool X8L = true;
+    if (rg == 1) {                                          // (timeline of the 16-row form)
+      if (g_fewtok_mode - 16 != 128) return false;
+      go(k_gemm_4bit_fewtok<T, 1, 1, true, true, 8, X8L, 128>, 8);
+      return true;
+    }
+    if (rg != 3) return false;
     switch (g_fewtok_mode - 16) {
       case 1: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 1>, 8); break;
       case 2: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 2>, 8); break;
@@ -470,6 +501,9 @@ bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uin
       case 71: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 71>, 8); break;
       case 128: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 128>, 8); break;
       case 135: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 135>, 8); break;
+      case 132: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 132>, 8); break;
+      case 192: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 192>, 8); break;
+      case 129: go(k_gemm_4bit_fewtok<T, 3, 1, true, true, 8, X8L, 129>, 8); break;
       default: return false;
     }
     return true;

@@ -15,7 +15,7 @@ m = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 extra = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 dev = torch.device("cuda", 0)
 gen = torch.Generator(device=dev).manual_seed(3)
-n_out, k_in = 11008, 4096
+n_out, k_in = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (11008, 4096)
 ws = []
 for _ in range(14):
     W = (torch.randn(n_out, k_in, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
@@ -24,7 +24,8 @@ for _ in range(14):
 x = torch.randn(m, k_in, device=dev, dtype=torch.bfloat16, generator=gen)
 out = torch.empty(m, n_out, device=dev, dtype=torch.bfloat16)
 F.GEMM_4BIT_GEMV_TOKENS = 1
-nwg = (n_out + 47) // 48
+rows_per_wg = 48 if n_out > 16 * 256 else 16
+nwg = (n_out + rows_per_wg - 1) // rows_per_wg
 buf = torch.zeros(nwg * 8 * 8, dtype=torch.int64, device=dev)
 F.set_fewtok_mode(16 + 128 + extra)
 for it in range(3):
@@ -49,3 +50,11 @@ for i, nm in enumerate(names):
         continue
     v = (v - t0) / 100.0
     print(f"  {nm:14s} {np.percentile(v, 5):6.2f} {np.percentile(v, 50):6.2f} {np.percentile(v, 95):6.2f} {v.max():6.2f}")
+tw = buf.view(nwg, 8, 8).cpu().numpy().astype(np.int64)
+live = tw[:, :, 0].min(axis=1) > 0
+st = tw[live, :, 0]
+wg_start = (st.min(axis=1) - t0) / 100.0
+intra = (st.max(axis=1) - st.min(axis=1)) / 100.0
+print(f"  workgroup start (first wave) p5/p50/p95/max {np.percentile(wg_start, 5):.2f} {np.percentile(wg_start, 50):.2f} "
+      f"{np.percentile(wg_start, 95):.2f} {wg_start.max():.2f}; spread of starts within a workgroup p50/max "
+      f"{np.percentile(intra, 50):.2f} {intra.max():.2f}")
