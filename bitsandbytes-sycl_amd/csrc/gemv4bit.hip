@@ -410,10 +410,14 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
 // K > GV_MAX_K does not fit its LDS activation copy; here the activations come from L2 (each workgroup reads all
 // of x) and only the pair table sits in LDS (the 128-B-stride copies of k_gemv_4bit_dot, conflict-free).  Same
 // per-chunk arithmetic as the other table kernels; the chunk-to-lane grouping, and so the fp32 summation order, differs.
+// R > 1 (round 3): R rows per workgroup (at most 4 waves), sharing one activation load and one table fill -- each
+// workgroup reads all of x from L2, so one row per workgroup moved 4x the weight bytes again as activations at
+// 1024 x 28672; every row's chunk grouping and summation order is unchanged (bit-identical to R = 1).
 constexpr int GW_MAX_WAVES = 16;
+constexpr int GW_MAX_WAVES_R = 4;                                   // (R > 1)
 
-template <typename T, int U, bool NESTED>
-__global__ void __launch_bounds__(GW_MAX_WAVES * 64)
+template <typename T, int U, bool NESTED, int R = 1>
+__global__ void __launch_bounds__((R > 1 ? GW_MAX_WAVES_R : GW_MAX_WAVES) * 64)
 k_gemv_4bit_wide(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
                  const float* __restrict__ datatype, T* __restrict__ out, int ldb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
@@ -423,24 +427,36 @@ k_gemv_4bit_wide(int M, int K, const T* __restrict__ A, const uint8_t* __restric
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int NT = blockDim.x, NW = NT >> 6;
-  const int row = blockIdx.x;
+  const int row0 = blockIdx.x * R;
   const int nch = K >> 5;
   const long long two_ldb = 2LL * ldb;
   auto chunk_of = [&](int u) { return min(tid + NT * u, nch - 1); };
-  // (1) statistics, activations (L2), then the weights (non-temporal)
-  float am[U];
-  uint32_t q8[U];
-  float a2[U];
+  auto row_of = [&](int j) { return min(row0 + j, M - 1); };
+  // (1) code values (scalar) and the nested code map first: loaded later, inside the table fill, they queued behind
+  //     the whole weight stream (1024 x 28672: 10.1 us); then statistics, activations (L2), the weights (non-temporal)
+  float dt[16];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const long long blk = (two_ldb * row + 32LL * chunk_of(u)) >> st.bs_shift;
-    if constexpr (NESTED) {
-      q8[u] = st.q8[blk];
-      a2[u] = st.absmax2[blk >> st.bs2_shift];
-    } else {
-      am[u] = st.absmax[blk];
-    }
+  for (int j = 0; j < 16; ++j) dt[j] = datatype[j];
+  float c2p[4] = {0.f, 0.f, 0.f, 0.f};                   // code2[tid + NT q], q < 256 / NT (NT >= 64)
+  if constexpr (NESTED) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c2p[q] = st.code2[min(tid + NT * q, 255)];
   }
+  float am[R][U];
+  uint32_t q8[R][U];
+  float a2[R][U];
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long blk = (two_ldb * row_of(j) + 32LL * chunk_of(u)) >> st.bs_shift;
+      if constexpr (NESTED) {
+        q8[j][u] = st.q8[blk];
+        a2[j][u] = st.absmax2[blk >> st.bs2_shift];
+      } else {
+        am[j][u] = st.absmax[blk];
+      }
+    }
   float offset = 0.0f;
   if constexpr (NESTED) offset = *st.offset;
   uint4 xv[U][4];
@@ -450,34 +466,50 @@ k_gemv_4bit_wide(int M, int K, const T* __restrict__ A, const uint8_t* __restric
     for (int q = 0; q < 4; ++q) xv[u][q] = reinterpret_cast<const uint4*>(A + 32 * chunk_of(u))[q];
   uintptr_t bp = (uintptr_t)B;
   asm volatile("" : "+s"(bp)::"memory");
-  uint4 b[U];
+  uint4 b[R][U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const u32x4_t v = __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row * ldb + 16LL * chunk_of(u)));
-    b[u] = make_uint4(v.x, v.y, v.z, v.w);
-  }
+  for (int j = 0; j < R; ++j)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u32x4_t v = __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row_of(j) * ldb + 16LL * chunk_of(u)));
+      b[j][u] = make_uint4(v.x, v.y, v.z, v.w);
+    }
   // (2) table: 16-B store i holds entry i >> 3 for copies 4 (i & 7) .. 4 (i & 7) + 3 (entry e of copy j at 128 e + 4 j)
   for (int i = tid; i < GV_TABLE_BYTES / 16; i += NT) {
     const int e = i >> 3;
-    const uint32_t v = Dot2<T>::pair(datatype[e >> 4], datatype[e & 15]);
+    float hi = dt[0], lo = dt[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      hi = (e >> 4) == j ? dt[j] : hi;
+      lo = (e & 15) == j ? dt[j] : lo;
+    }
+    const uint32_t v = Dot2<T>::pair(hi, lo);
     *reinterpret_cast<uint4*>(table + 16 * i) = make_uint4(v, v, v, v);
   }
-  if constexpr (NESTED)
-    for (int t = tid; t < 256; t += NT) code2s[t] = st.code2[t];
+  if constexpr (NESTED) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (tid + NT * q < 256) code2s[tid + NT * q] = c2p[q];
+  }
   __syncthreads();
   if constexpr (NESTED) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) am[u] = __fadd_rn(__fmul_rn(code2s[q8[u]], a2[u]), offset);
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) am[j][u] = __fadd_rn(__fmul_rn(code2s[q8[j][u]], a2[j][u]), offset);
   }
   // (3) dot: per chunk s0 / s1 chains of v_dot2 over 16 packed bytes, scaled by the chunk's absmax
   const uint32_t lane4 = (lane & 31) * 4;
+  float accs[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
   float acc = 0.0f;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t x[16] = {xv[u][0].x, xv[u][0].y, xv[u][0].z, xv[u][0].w, xv[u][1].x, xv[u][1].y, xv[u][1].z,
                             xv[u][1].w, xv[u][2].x, xv[u][2].y, xv[u][2].z, xv[u][2].w, xv[u][3].x, xv[u][3].y,
                             xv[u][3].z, xv[u][3].w};
-    const uint32_t w[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
+    const uint32_t w[4] = {b[j][u].x, b[j][u].y, b[j][u].z, b[j][u].w};
     uint32_t l[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
@@ -488,16 +520,19 @@ k_gemv_4bit_wide(int M, int K, const T* __restrict__ A, const uint8_t* __restric
       s0 = Dot2<T>::dot(x[i], l[i], s0);
       s1 = Dot2<T>::dot(x[i + 1], l[i + 1], s1);
     }
-    const float part = (s0 + s1) * am[u];
+    const float part = (s0 + s1) * am[j][u];
     acc += (tid + NT * u < nch) ? part : 0.0f;
   }
-  acc = wave_sum(acc);
-  if (lane == 0) red[wave] = acc;
+  accs[j] = wave_sum(acc);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < R; ++j) red[wave * R + j] = accs[j];
   __syncthreads();
-  if (tid == 0) {
-    float s = red[0];
-    for (int w2 = 1; w2 < NW; ++w2) s += red[w2];
-    out[row] = Io<T>::from_f32(s);
+  if (tid < R && row0 + tid < M) {
+    float s = red[tid];
+    for (int w2 = 1; w2 < NW; ++w2) s += red[w2 * R + tid];
+    out[row0 + tid] = Io<T>::from_f32(s);
   }
 }
 
@@ -524,6 +559,7 @@ k_gemv_4bit_generic(int M, int K, const T* __restrict__ A, const uint8_t* __rest
 // 1 = k_gemv_4bit_dot only, 2 = k_gemv_4bit_wide wherever it applies, 3 = auto without the wide kernel (A/B, tests);
 // 20 + U: the wide kernel with U chunks per lane (lab)
 int g_gemv_kernel = 0;
+int g_gemv_wide_rows = 0;   // 1: the wide kernel one row per workgroup (A/B, tests)
 
 int device_cu_count() {
   static int cus = 0;
@@ -601,11 +637,29 @@ static bool launch_gemv_wide(int m, int k, const T* A, const uint8_t* B, const G
   }
   if (U > 4) return false;
   nw = (nch + 64 * U - 1) / (64 * U);
-  const size_t lds = GV_TABLE_BYTES + 256 * sizeof(float) + GW_MAX_WAVES * sizeof(float);
+  // rows per workgroup: as many as keep >= one workgroup per CU (at most 4, and only with <= 4 waves)
+  int R = std::max(1, std::min(4, m / device_cu_count()));
+  if (nw > GW_MAX_WAVES_R || g_gemv_wide_rows == 1 || (U != 1 && U != 4)) R = 1;
+  const size_t lds = GV_TABLE_BYTES + 256 * sizeof(float) + GW_MAX_WAVES * 4 * sizeof(float);
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)m), dim3(64 * nw), lds, current_stream(), m, k, A, B, st, datatype, out, ldb);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((m + R - 1) / R)), dim3(64 * nw), lds, current_stream(), m, k, A, B, st,
+                       datatype, out, ldb);
     return true;
   };
+  if (R > 1 && U == 4) {
+    switch (R) {
+      case 2: return go(k_gemv_4bit_wide<T, 4, NESTED, 2>);
+      case 3: return go(k_gemv_4bit_wide<T, 4, NESTED, 3>);
+      default: return go(k_gemv_4bit_wide<T, 4, NESTED, 4>);
+    }
+  }
+  if (R > 1 && U == 1) {
+    switch (R) {
+      case 2: return go(k_gemv_4bit_wide<T, 1, NESTED, 2>);
+      case 3: return go(k_gemv_4bit_wide<T, 1, NESTED, 3>);
+      default: return go(k_gemv_4bit_wide<T, 1, NESTED, 4>);
+    }
+  }
   switch (U) {
     case 1: return go(k_gemv_4bit_wide<T, 1, NESTED>);
     case 2: return go(k_gemv_4bit_wide<T, 2, NESTED>);
@@ -701,6 +755,8 @@ extern "C" {
 
 // [additive, testing] 0 = auto (k_gemv_4bit_bal where it fits), 1 = the 4-waves-x-R-rows kernel only
 void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
+// [additive, testing] 1 = the wide GEMV one row per workgroup (the round-2 form); 0 = rows per workgroup by the rule
+void cgemv_4bit_set_wide_rows(int mode) { bnb::g_gemv_wide_rows = mode; }
 // [lab, not in the header] LDS bytes up to which the balanced GEMV runs two workgroups per CU (default 80 KiB)
 void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size_t)bytes; }
 

@@ -565,7 +565,7 @@ def test_gemv_balanced_kernel_matches_dot_kernel(dev, dtype, nested, shape, quan
                                    (1000, 4096)])
 @pytest.mark.parametrize("quant", [("nf4", 64), ("fp4", 128)])
 def test_gemv_wide_kernel(dev, dtype, shape, quant):
-    """k_gemv_4bit_wide (one workgroup per row, K split over its waves, summed in wave order): the default for K
+    """k_gemv_4bit_wide (1..4 rows per workgroup, K split over its waves, summed in wave order): the default for K
     beyond the balanced kernel's LDS and for fewer rows than CUs, forced here on every shape (1000 x 4096 would take
     the balanced kernel).  Within the oracle tolerance for plain and compressed statistics, the in-kernel decode
     bit-identical to the decoded-absmax call, and the default route equal to the forced one where it is taken."""
@@ -586,6 +586,11 @@ def test_gemv_wide_kernel(dev, dtype, shape, quant):
         F.lib.cgemv_4bit_set_kernel(2)
         try:
             y = F.gemv_4bit(x, q.t(), state=st)
+            F.lib.cgemv_4bit_set_wide_rows(1)       # one row per workgroup: the rows-per-workgroup form is bit-equal
+            try:
+                y_r1 = F.gemv_4bit(x, q.t(), state=st)
+            finally:
+                F.lib.cgemv_4bit_set_wide_rows(0)
             two_step = torch.empty_like(y)
             getattr(F.lib, f"cgemm_4bit_inference_naive_{name}")(
                 ct.c_int32(N), ct.c_int32(1), ct.c_int32(K), F.get_ptr(x), F.get_ptr(q), F.get_ptr(absmax),
@@ -597,6 +602,7 @@ def test_gemv_wide_kernel(dev, dtype, shape, quant):
         frac, err = _close(y.float().cpu().numpy()[0], exp, tol, tol)
         assert frac == 0.0, (nested, err)
         assert torch.equal(y.view(torch.int16), two_step.view(torch.int16))
+        assert torch.equal(y.view(torch.int16), y_r1.view(torch.int16))
         if K > 16384 or N < 256:
             assert torch.equal(y_default.view(torch.int16), y.view(torch.int16))
 
