@@ -14,7 +14,7 @@ from python_src_quants import functional as F  # noqa: E402
 
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(5)
-SHAPES = [(1280, 8192), (1024, 8192), (7168, 8192), (1024, 28672)]
+SHAPES = [tuple(int(v) for v in t.split('x')) for t in os.environ.get('DP_SHAPES', '1280x8192,1024x8192,7168x8192,1024x28672').split(',')]
 COPIES = 8
 
 
@@ -53,7 +53,12 @@ for n, k in SHAPES:
     F.set_fewtok_mode(1)
     t = graph_us([lambda q=q, st=st: F.gemv_4bit(x, q.t(), out=out, state=st) for q, st in ws])
     line += f"  gemv_4bit {t:6.2f} us ({wbytes / t / 1e3:5.0f} GB/s)"
-    if F.lib.cgemm_4bit_fewtok_takes(n, 1, k, 64) or True:
+    if os.environ.get("DP_WIDE"):
+        F.lib.cgemv_4bit_set_kernel(2)
+        tw = graph_us([lambda q=q, st=st: F.gemv_4bit(x, q.t(), out=out, state=st) for q, st in ws])
+        F.lib.cgemv_4bit_set_kernel(0)
+        line += f"  wide(forced) {tw:6.2f} us"
+    if not os.environ.get("DP_WIDE"):
         F.set_fewtok_mode(2)
         t2 = graph_us([lambda q=q, st=st: F.gemm_4bit(x, q, st, out=out) for q, st in ws])
         line += f"  fewtok(forced) {t2:6.2f} us"
