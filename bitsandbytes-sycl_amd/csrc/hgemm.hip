@@ -144,6 +144,9 @@ __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r
 //   vmcnt wait, 128 / 256 = no barrier B2 / B1, 512 = register-staged copies (slower: 256 vs 242 us), 1024 = no
 //   copies, 2048 = no fragment re-reads (profiles/lab/r03_hgemm_ablation.txt).  Launched: 8 + 16 + 4096.
 constexpr int HG_V = 8 + 16 + 4096;
+// A/B arm selectable at run time (chgemm_set_variant(1)): the three-barrier operand-split schedule (V & 8192)
+constexpr int HG_V_ALT = 16 + 8192;
+static int g_hgemm_variant = 0;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
 // SPLIT (bf16 / fp16 only): the split-K form -- its epilogue stores fp32 partials only.  A separate instantiation, so
 // that each kernel has ONE epilogue reading the accumulators (two in one kernel made the allocator spill).
@@ -360,6 +363,70 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     }
   };
 
+  // V & 8192: the operand-split schedule, three barriers per k-tile (128 MFMAs), MFMA index q:
+  //   q 0..14   this wave reads step 1's B fragments (w1) of the stage, one per 2 MFMAs;
+  //   q 21      lgkmcnt(0) + barrier B1: every wave is done with the stage's B rows, so tile t+2's B pieces go into
+  //             them from q 24 on (5 before B2, 3 after), while this wave reads step 1's A fragments (x1, q 23..44);
+  //   q 50      lgkmcnt(0) + barrier B2: the stage's A rows are free too; tile t+2's A pieces from q 64 on;
+  //   q 88      vmcnt(13) (the 13 pieces issued so far in this k-tile may still fly: tile t+1, issued one k-tile
+  //             earlier, has landed for this wave) + barrier B3 (... for every wave); tile t+1's step-0 fragments are
+  //             read under the remaining 39 MFMAs (one per 2), beside the last 3 A pieces.
+  // So a piece is issued as soon as its rows are free (from MFMA 24 instead of 64) and 13 of 16 stay in flight across
+  // the tile boundary; the fragment reads of a k-tile never share an MFMA gap with more than one DMA issue.
+  auto tile3 = [&](auto first, auto last, int t) {
+    constexpr bool FIRST = decltype(first)::value, L = decltype(last)::value;
+    const int st = t & 1;
+    const int kn = min(t + 2, nk - 1);
+    const uint32_t base = lds0 + st * HG_STAGE;
+    // compile-time schedule (q is a constant after the unroll)
+    constexpr int B1 = 21, B2 = 50, B3 = 88;
+    auto b_piece = [](int q) -> int {   // B piece issued after MFMA q, or -1
+      return q == 24 ? 0 : q == 28 ? 1 : q == 32 ? 2 : q == 36 ? 3 : q == 40 ? 4 : q == 52 ? 5 : q == 56 ? 6
+                                                                                                        : q == 60 ? 7 : -1;
+    };
+    auto a_piece = [](int q) -> int {   // A piece issued after MFMA q, or -1
+      return q == 64 ? 0 : q == 68 ? 1 : q == 72 ? 2 : q == 76 ? 3 : q == 80 ? 4 : q == 97 ? 5 : q == 107 ? 6
+                                                                                                         : q == 117 ? 7 : -1;
+    };
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+      const int j = q >> 3, i = q & 7;
+      if constexpr (FIRST) acc[j][i] = Op::mma0(w0[j], x0[i]);
+      else acc[j][i] = Op::mma(w0[j], x0[i], acc[j][i]);
+      if (q < 16 && (q & 1) == 0) w1[q >> 1] = rd(st, wo1, q >> 1);
+      if (q >= 23 && q <= 44 && (q - 23) % 3 == 0) x1[(q - 23) / 3] = rd(st, xo1, (q - 23) / 3);
+      if constexpr (!L) {
+        if (q == 22) hg_set_m0(base + HG_TILE);
+        if (b_piece(q) >= 0) glds16_chain<1024>(B + (long long)kn * 128, boff[b_piece(q)]);
+        if (q == 61) hg_set_m0(base);
+      }
+      if (q == B1 || q == B2) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0)
+        if constexpr (!L) __builtin_amdgcn_s_barrier();
+      }
+      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int q = 64; q < 128; ++q) {
+      const int j = (q - 64) >> 3, i = q & 7;
+      acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
+      if constexpr (!L) {
+        if (a_piece(q) >= 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[a_piece(q)]);
+        if (q == B3) {
+          asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        if (q > B3 && q <= B3 + 31 && ((q - B3 - 1) & 1) == 0) {
+          const int r = (q - B3 - 1) >> 1;               // 0..15: w0[0], x0[0..7], w0[1..7] (the order of their use)
+          if (r == 0) w0[0] = rd(st ^ 1, wo0, 0);
+          else if (r <= 8) x0[r - 1] = rd(st ^ 1, xo0, r - 1);
+          else w0[r - 8] = rd(st ^ 1, wo0, r - 8);
+        }
+      }
+      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   // ---- prologue: tiles 0 and 1 in flight, tile 0 landed, its step-0 fragments in registers
   if constexpr (RS) {
 #pragma unroll
@@ -381,12 +448,22 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
 #pragma unroll
   for (int f = 0; f < 8; ++f) { w0[f] = rd(0, wo0, f); x0[f] = rd(0, xo0, f); }
 
-  half1(std::true_type{}, 0);
-  for (int t = 0; t + 1 < nk; ++t) {
-    half2(std::false_type{}, t, t & 1);
-    half1(std::false_type{}, t + 1);
+  if constexpr ((V & 8192) != 0) {
+    if (nk == 1) {
+      tile3(std::true_type{}, std::true_type{}, 0);
+    } else {
+      tile3(std::true_type{}, std::false_type{}, 0);
+      for (int t = 1; t + 1 < nk; ++t) tile3(std::false_type{}, std::false_type{}, t);
+      tile3(std::false_type{}, std::true_type{}, nk - 1);
+    }
+  } else {
+    half1(std::true_type{}, 0);
+    for (int t = 0; t + 1 < nk; ++t) {
+      half2(std::false_type{}, t, t & 1);
+      half1(std::false_type{}, t + 1);
+    }
+    half2(std::true_type{}, nk - 1, (nk - 1) & 1);
   }
-  half2(std::true_type{}, nk - 1, (nk - 1) & 1);
   wait_vmcnt0();                                          // no LDS-DMA may outlive the workgroup
   // MFMA (asm, invisible to hipcc's hazard recognizer) -> v_accvgpr_read: pad the wait states by hand
   __builtin_amdgcn_sched_barrier(0);
@@ -396,7 +473,10 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   // ---- epilogue: acc[j][i][r] = C[m0 + 128 wm + 16 i + fr][n0 + 128 wn + 16 j + 4 fg + r] -- four consecutive
   // columns of one row per accumulator: one 8-B store (16-bit outputs) or 16-B store (int32).  Full tiles (the common
   // case) store unconditionally; edge tiles check every row / column.
-  const int mb = m0 + 128 * wm + fr, nb = n0 + 128 * wn + 4 * fg;
+  // (the lane's fragment row / group recomputed from mbcnt, not kept live from the prologue: at 256 VGPRs the main
+  // loop has no register to spare for them)
+  const int lane_e = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int mb = m0 + 128 * wm + (lane_e & 15), nb = n0 + 128 * wn + 4 * (lane_e >> 4);
   constexpr int OUT = (OP == HG_I8_I32) ? 4 : 2;
   const bool full = (m0 + HG_BM <= M) && (n0 + HG_BN <= N) && (((ldc * OUT) & 15) == 0) &&
                     (((uintptr_t)Cv & 15) == 0);
@@ -432,10 +512,23 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     // (direct 8-B fragment stores put 16 rows x 32 B in one instruction: +4 us of epilogue per launch at 4096^2)
     __syncthreads();                                   // every wave is past its last stage read
     uint8_t* ep = smem + wave * (128 * HG_EPI_PITCH);
+    // HG_I8_DEQ: the lane's row / column statistics and bias loaded once, up front (the fragment registers are free
+    // now): 8 row scales, 8 x 4 column scales (16-B loads: nb % 4 == 0) and 8 x 4 bias halves.  Loading them per
+    // accumulator (256 dependent L1 loads per lane) cost ~24 us of fixed epilogue per launch.
+    float rsv[8];
+    f32x4_t csv[8];
+    uint2 bsv[8];
+    if constexpr (OP == HG_I8_DEQ) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rsv[i] = rowStats[mb + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        csv[j] = *reinterpret_cast<const f32x4_t*>(colStats + nb + 16 * j);
+        bsv[j] = bias ? *reinterpret_cast<const uint2*>(bias + nb + 16 * j) : make_uint2(0u, 0u);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float rs = 0.f;
-      if constexpr (OP == HG_I8_DEQ) rs = rowStats[mb + 16 * i];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         uint2 v;
@@ -444,15 +537,16 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
           v.x = cvt_pk<T>(acc[j][i][0], acc[j][i][1]);
           v.y = cvt_pk<T>(acc[j][i][2], acc[j][i][3]);
         } else if constexpr (OP == HG_I8_DEQ) {
-          const int n = nb + 16 * j;
           uint16_t h[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            h[r] = __builtin_bit_cast(uint16_t, mm_dequant_value(acc[j][i][r], rs, colStats[n + r],
-                                                                 bias ? (float)bias[n + r] : 0.0f));
+          for (int r = 0; r < 4; ++r) {
+            const uint16_t bh = (uint16_t)((r < 2 ? bsv[j].x : bsv[j].y) >> (16 * (r & 1)));
+            h[r] = __builtin_bit_cast(uint16_t, mm_dequant_value(acc[j][i][r], rsv[i], csv[j][r],
+                                                                 (float)__builtin_bit_cast(fp16_t, bh)));
+          }
           v = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
         }
-        *reinterpret_cast<uint2*>(ep + (16 * i + fr) * HG_EPI_PITCH + 2 * (16 * j + 4 * fg)) = v;
+        *reinterpret_cast<uint2*>(ep + (16 * i + (lane_e & 15)) * HG_EPI_PITCH + 2 * (16 * j + 4 * (lane_e >> 4))) = v;
         __builtin_amdgcn_sched_barrier(0);   // one accumulator at a time: no VGPR burst that displaces AGPRs
       }
     }
@@ -460,7 +554,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     uint8_t* cbase = reinterpret_cast<uint8_t*>(Cv) + ((long long)(m0 + 128 * wm) * ldc + n0 + 128 * wn) * 2;
 #pragma unroll 8
     for (int it = 0; it < 32; ++it) {
-      const int row = 4 * it + (lane >> 4), c16 = lane & 15;
+      const int row = 4 * it + (lane_e >> 4), c16 = lane_e & 15;
       const uint4 v = *reinterpret_cast<const uint4*>(ep + row * HG_EPI_PITCH + 16 * c16);
       *reinterpret_cast<uint4*>(cbase + (long long)row * ldc * 2 + 16 * c16) = v;
     }
@@ -543,6 +637,8 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
                  const float* rowStats = nullptr, const float* colStats = nullptr, const fp16_t* bias = nullptr,
                  float* ws = nullptr, long long ws_bytes = 0) {
   if (!hgemm_fits(m, n, k, lda, ldb, A, B, HgOpT<OP>::ELEM) || ldc < n) return 1;
+  // the dequant epilogue reads 4 column scales / 4 bias halves per 16-B / 8-B load
+  if (OP == HG_I8_DEQ && (((uintptr_t)colStats & 15) || ((uintptr_t)bias & 7))) return 1;
   HgSplit sp{1, (int)((long long)k * HgOpT<OP>::ELEM / 128)};
   if constexpr (OP == HG_BF16 || OP == HG_FP16) {
     const HgSplit want = hgemm_split(m, n, k, HgOpT<OP>::ELEM);
@@ -551,10 +647,19 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
       sp = want;
   }
   if (sp.splits > 1) {
-    if constexpr (OP == HG_BF16 || OP == HG_FP16)
-      hipLaunchKernelGGL((k_hgemm<OP, HG_V, true>), dim3((unsigned)(hgemm_tiles(m, n) * sp.splits)), dim3(HG_THREADS), 0,
-                         current_stream(), m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sp.splits,
-                         sp.kchunk);
+    if constexpr (OP == HG_BF16 || OP == HG_FP16) {
+      if (g_hgemm_variant == 1)
+        hipLaunchKernelGGL((k_hgemm<OP, HG_V_ALT, true>), dim3((unsigned)(hgemm_tiles(m, n) * sp.splits)), dim3(HG_THREADS),
+                           0, current_stream(), m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sp.splits,
+                           sp.kchunk);
+      else
+        hipLaunchKernelGGL((k_hgemm<OP, HG_V, true>), dim3((unsigned)(hgemm_tiles(m, n) * sp.splits)), dim3(HG_THREADS),
+                           0, current_stream(), m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sp.splits,
+                           sp.kchunk);
+    }
+  } else if (g_hgemm_variant == 1) {
+    hipLaunchKernelGGL((k_hgemm<OP, HG_V_ALT>), dim3((unsigned)hgemm_tiles(m, n)), dim3(HG_THREADS), 0, current_stream(),
+                       m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, sp.kchunk);
   } else {
     hipLaunchKernelGGL((k_hgemm<OP, HG_V>), dim3((unsigned)hgemm_tiles(m, n)), dim3(HG_THREADS), 0, current_stream(), m,
                        n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, sp.kchunk);
@@ -608,5 +713,11 @@ int chgemm_tn_ws_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_
   return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
 }
 long long chgemm_tn_workspace_bytes(int m, int n, int k) { return bnb::hgemm_workspace_bytes(m, n, k, 2); }
+// [additive, testing] k_hgemm schedule: 0 = the default, 1 = the A/B arm (HG_V_ALT); returns the previous setting
+int chgemm_set_variant(int v) {
+  const int prev = bnb::g_hgemm_variant;
+  bnb::g_hgemm_variant = v;
+  return prev;
+}
 
 }  // extern "C"

@@ -131,9 +131,24 @@ def shard_int8_rows(CB: torch.Tensor, SCB: torch.Tensor, world: int, rank: int):
     return CB[start:end], SCB[start:end]
 
 
+# At world 1 the gathers below are skipped (the slice IS the output).  set_force_collective(True) runs them anyway
+# through the initialised process group -- so a one-GPU box exercises the RCCL all-gather, its async overlap and its
+# HIP-graph capture exactly as the multi-GPU step does (tests/test_rccl_gpu.py).
+_FORCE_COLLECTIVE = [False]
+
+
+def set_force_collective(on: bool) -> None:
+    """Run the all-gathers even at world size 1 (needs an initialised process group); test / rehearsal knob."""
+    _FORCE_COLLECTIVE[0] = bool(on)
+
+
+def _collective(world: int) -> bool:
+    return world > 1 or (_FORCE_COLLECTIVE[0] and dist.is_available() and dist.is_initialized())
+
+
 def gather_columns(y_local: torch.Tensor, world: int, group=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """All-gather the per-rank [M, n] slices into [world, M, n] (one collective; RCCL on GPU)."""
-    if world == 1:
+    if not _collective(world):
         return y_local.unsqueeze(0)
     y_local = y_local.contiguous()
     if out is None:
@@ -172,7 +187,7 @@ def sharded_forward_overlapped(x2: torch.Tensor, local_mm: Callable, world: int,
         yc = local_mm(x2[rows], None if y is None else y[rows])
         if out is None:
             out = torch.empty((chunks, world, Mc, yc.shape[1]), dtype=yc.dtype, device=yc.device)
-        if world == 1:
+        if not _collective(world):
             out[c, 0].copy_(yc)
         else:
             works.append(_gather_async(out[c], yc.contiguous(), group))
@@ -181,7 +196,7 @@ def sharded_forward_overlapped(x2: torch.Tensor, local_mm: Callable, world: int,
         if rows_out is not None:
             rows_out[c * Mc:(c + 1) * Mc].view(Mc, world, -1).copy_(out[c].permute(1, 0, 2))
     if rows_out is not None:
-        if world == 1:
+        if not works:
             rows_out.copy_(out.reshape(rows_out.shape))
         return rows_out
     return out
@@ -289,7 +304,7 @@ class ShardedDecode:
         """One eager decode step on the static buffers; returns `rows`."""
         self.local_fn(self.x, self.y)
         gather_columns(self.y, self.world, self.group, out=self.gathered)
-        if self.world == 1:
+        if not _collective(self.world):
             self.gathered[0].copy_(self.y)
         self.rows.view(1, self.world, -1).copy_(self.gathered.permute(1, 0, 2))
         return self.rows
@@ -297,7 +312,7 @@ class ShardedDecode:
     def capture(self, warmup: int = 2) -> bool:
         """Capture step() into a HIP graph (side-stream warm-up first, as torch.cuda.graph requires).  Returns False
         (and leaves eager mode) when the backend cannot be captured (gloo, or a collective capture refused)."""
-        if not self.x.is_cuda or (self.world > 1 and dist.get_backend(self.group) == "gloo"):
+        if not self.x.is_cuda or (_collective(self.world) and dist.get_backend(self.group) == "gloo"):
             return False
         s = torch.cuda.Stream(device=self.x.device)
         s.wait_stream(torch.cuda.current_stream(self.x.device))

@@ -207,3 +207,46 @@ def test_hgemm_split_k_against_fp32_product(dev, dtype, mnk):
     rc, Yu = _hgemm(F, X, W)                        # the plain entry point runs the unsplit kernel
     torch.cuda.synchronize()
     assert torch.equal(Yu, outs[2])
+
+
+@pytest.mark.parametrize("mnk", [(4096, 4096, 11008), (1000, 1100, 4096), (257, 513, 64), (300, 260, 128),
+                                 (512, 768, 192), (4096, 1024, 28672)])
+def test_hgemm_schedule_variants_bit_identical(dev, mnk):
+    """The alternative k_hgemm schedule (chgemm_set_variant(1): three barriers per k-tile, operand-split DMA) runs
+    every accumulator's MFMAs in the same k order as the default, so bf16 / fp16 outputs (split-K included) and the
+    int8 4-wave igemmlt + dequant are bit-identical to the default arm; 1, 2 and 3 k-tiles cover its first / last-tile
+    forms."""
+    F = _F()
+    m, n, k = mnk
+    g = torch.Generator(device=dev).manual_seed(m + 3 * n + k)
+    for dtype in (torch.bfloat16, torch.float16):
+        X = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(dtype)
+        W = (torch.rand(n, k, device=dev, generator=g) * 2 - 1).to(dtype)
+        outs = []
+        for v in (0, 1):
+            prev = F.lib.chgemm_set_variant(v)
+            try:
+                rc, Y = _hgemm_ws(F, X, W)
+                torch.cuda.synchronize()
+            finally:
+                F.lib.chgemm_set_variant(prev)
+            assert rc == 0
+            outs.append(Y)
+        _check(outs[1], X, W)
+        assert torch.equal(outs[0], outs[1])
+    A = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8, generator=g)
+    B = torch.randint(-127, 128, (n, k), device=dev, dtype=torch.int8, generator=g)
+    rs = torch.rand(m, device=dev, generator=g) * 2 + 0.5
+    cs = torch.rand(n, device=dev, generator=g) * 2 + 0.5
+    bias = torch.randn(n, device=dev, generator=g).half()
+    res = {}
+    for tile, v in ((0, 0), (4, 0), (4, 1)):
+        F.lib.cigemm_set_tile(tile)
+        prev = F.lib.chgemm_set_variant(v)
+        try:
+            res[(tile, v)] = F.igemmlt_dequant(A, B, rs, cs, bias=bias)
+            torch.cuda.synchronize()
+        finally:
+            F.lib.chgemm_set_variant(prev)
+            F.lib.cigemm_set_tile(0)
+    assert torch.equal(res[(0, 0)], res[(4, 0)]) and torch.equal(res[(0, 0)], res[(4, 1)])
