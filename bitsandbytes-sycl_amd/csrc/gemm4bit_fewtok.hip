@@ -434,6 +434,7 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
 // 0 = auto, 1 = off, 2 = forced wherever it fits (A/B knob; tests); >= 16: lab ablations
 int g_fewtok_mode = 0;
 extern int g_fewtoken_kernel;   // gemm4bit_wk.hip: != 0 selects one of the older few-token kernels
+int skinny_cfg_knob();          // gemm4bit_skinny.hip: >= 0 forces a split-K geometry (lab A/B)
 
 bool fewtok_applicable(int m, int n, int k, int lda, int ldb, int blocksize, const void* A, const void* B) {
   return g_fewtok_mode != 1 && n >= 1 && n <= 32 && m >= 1 && k >= 64 && k % 64 == 0 && 2LL * ldb >= k &&
@@ -564,8 +565,11 @@ void cgemm_4bit_set_fewtok_mode(int mode) { bnb::g_fewtok_mode = mode; }
 // [additive] 1 when the 4-bit GEMM entry points run the whole-K few-token kernel for out features m, n activation rows,
 // in features k and this blocksize (the auto rule above, or the forced mode), else 0 -- the Python layer asks before
 // it sends 2..4 rows to the multi-row GEMV
+// (the launch's own conditions: a lab mode (>= 16), an older few-token kernel (g_fewtoken_kernel) or a forced split-K
+// geometry (g_skinny_cfg) each keep the launch off this kernel, so the answer is 0 for them too)
 int cgemm_4bit_fewtok_takes(int m, int n, int k, int blocksize) {
-  if (bnb::g_fewtok_mode == 1 || bnb::g_fewtoken_kernel != 0 || n < 1 || n > 32 || k < 64 || k % 64 || blocksize < 64 || (blocksize & (blocksize - 1)))
+  if (bnb::g_fewtok_mode == 1 || bnb::g_fewtok_mode >= 16 || bnb::g_fewtoken_kernel != 0 || bnb::skinny_cfg_knob() >= 0 ||
+      n < 1 || n > 32 || k < 64 || k % 64 || blocksize < 64 || (blocksize & (blocksize - 1)))
     return 0;
   return (bnb::g_fewtok_mode >= 2 || bnb::fewtok_auto_takes(m, n, k)) ? 1 : 0;
 }

@@ -282,6 +282,7 @@ bool skinny_applicable(int m, int n, int k, int lda, int ldb, int blocksize, con
 // g_skinny_cfg (cgemm_4bit_set_skinny_config, lab A/B): -1 = that rule, 0 = base, 1 = 8 waves same NB, 2 = 8 waves 2 x NB.
 static int g_skinny_cfg = -1;
 extern int g_fewtoken_kernel;   // gemm4bit_wk.hip
+int skinny_cfg_knob() { return g_skinny_cfg; }
 
 struct SkGeom {
   int cfg, waves, nb, splits;

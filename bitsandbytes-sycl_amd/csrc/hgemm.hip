@@ -9,7 +9,9 @@
 // is 16 ds_read_b128 per 64 MFMAs -- a third fewer LDS bytes per MFMA than the 8-wave 128 x 64 split
 // (MI355X_MICROARCH.md 'DVFS give-back': LDS read bytes cost clock).
 //
-// Pipeline: two LDS stages of 64 KiB (A and B tiles [256][64], 16-B slots XOR-swizzled by (row >> 1) & 7 through
+// Pipeline (round 4 default, V & 8192: see tile3 below -- three barriers per k-tile, each operand's DMA issued as soon
+// as its rows of the stage are free; the two-half form described next is the round-3 schedule, kept as an A/B arm):
+// two LDS stages of 64 KiB (A and B tiles [256][64], 16-B slots XOR-swizzled by (row >> 1) & 7 through
 // the DMA source address, conflict-free for the fragment reads).  Both operands move by LDS-DMA
 // (global_load_lds_dwordx4, scalar base + one 32-bit lane offset per piece, so ragged edges are clamped once in
 // the offsets and a k-step advances only the scalar base).  Per k-tile t, two halves:
@@ -143,9 +145,12 @@ __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r
 //   another 2-3 %, profiles/lab/r03_hgemm_m0_chain.txt).  Lab-only ablations (wrong results, timing only): 64 = no
 //   vmcnt wait, 128 / 256 = no barrier B2 / B1, 512 = register-staged copies (slower: 256 vs 242 us), 1024 = no
 //   copies, 2048 = no fragment re-reads (profiles/lab/r03_hgemm_ablation.txt).  Launched: 8 + 16 + 4096.
-constexpr int HG_V = 8 + 16 + 4096;
-// A/B arm selectable at run time (chgemm_set_variant(1)): the three-barrier operand-split schedule (V & 8192)
-constexpr int HG_V_ALT = 16 + 8192;
+// Round 4: the three-barrier operand-split schedule (V & 8192, tile3 below) is the launched one: bit-identical to the
+// two-half schedule and 0.8-1.5 % faster at 4096 x 4096 x 11008 (bf16 234.6-235.3 vs 236.6-238.6 us; int8 4-wave
+// 127.3-129.3 vs 128.7-129.3 us; tools/hgemm_variant_ab.py, profiles/lab/r04_hgemm_variants.txt).  The round-3
+// two-half schedule stays selectable at run time (chgemm_set_variant(1)) as the A/B arm.
+constexpr int HG_V = 16 + 8192;
+constexpr int HG_V_ALT = 8 + 16 + 4096;
 static int g_hgemm_variant = 0;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
 // SPLIT (bf16 / fp16 only): the split-K form -- its epilogue stores fp32 partials only.  A separate instantiation, so
@@ -618,14 +623,32 @@ constexpr int HG_SPLIT_TILES = 192, HG_SPLIT_MIN_KT = 8, HG_SPLIT_MAX = 8;
 struct HgSplit {
   int splits, kchunk;
 };
+int device_cu_count();   // CUs of the current device (cached; gemv4bit.hip)
+// The split count is chosen by its cost in k-tile times of one workgroup: rounds of workgroups on the CUs x the k-tiles
+// per split, plus the fp32 partials each extra split writes and the reduce reads back (8 bytes per output, at ~5 TB/s,
+// against ~1.37 us per k-tile).  Round 3's rule (splits = CUs / tiles) could overshoot the CU count by a few
+// workgroups -- 43 tiles x 6 = 258 workgroups, a second round for 2 of them (256 x 11008 x 4096: 89 us against 58 on
+// the library GEMM, tools/route_probe3.py, profiles/lab/r04_routes.txt).
 HgSplit hgemm_split(int m, int n, int k, int elem) {
   const long long tiles = hgemm_tiles(m, n);
   const int nkt = (int)((long long)k * elem / 128);
   if (tiles >= HG_SPLIT_TILES || n % 4) return HgSplit{1, nkt};
-  int s = (int)std::min<long long>(HG_SPLIT_MAX, (256 + tiles - 1) / tiles);
-  s = std::max(1, std::min(s, nkt / HG_SPLIT_MIN_KT));
-  const int kchunk = (nkt + s - 1) / s;
-  return HgSplit{(nkt + kchunk - 1) / kchunk, kchunk};
+  int cus = device_cu_count();
+  if (cus <= 0) cus = 256;
+  const double part_kt = (double)m * n * 8.0 / 5.0e12 / 1.37e-6;   // one split's partial traffic, in k-tile times
+  HgSplit best{1, nkt};
+  double best_cost = (double)((tiles + cus - 1) / cus) * nkt;
+  for (int s = 2; s <= HG_SPLIT_MAX; ++s) {
+    const int kchunk = (nkt + s - 1) / s;
+    if (kchunk < HG_SPLIT_MIN_KT) break;
+    const int splits = (nkt + kchunk - 1) / kchunk;
+    const double cost = (double)((tiles * splits + cus - 1) / cus) * kchunk + part_kt * splits;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = HgSplit{splits, kchunk};
+    }
+  }
+  return best;
 }
 long long hgemm_workspace_bytes(int m, int n, int k, int elem) {
   const HgSplit sp = hgemm_split(m, n, k, elem);

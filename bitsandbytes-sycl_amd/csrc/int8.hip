@@ -610,20 +610,23 @@ k_igemm(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restr
   }
 }
 
-static int g_igemm_tile = 0;   // 0 = auto, 128 = force the 128x128 register-staged kernel, 4 = the 4-wave
-                               // hgemm.hip kernel for row-major operands (tests / A-B)
+static int g_igemm_tile = 0;   // 0 = auto, 128 = force the 128x128 register-staged kernel, 4 = force the 4-wave
+                               // hgemm.hip kernel for row-major operands, 8 = force the 8-wave igemm_256 (tests / A-B)
 
 template <int AF, int BF, int EPI>
 static int launch_igemm(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, const float* row_scale, long long lda,
                         long long ldb, long long ldc, const float* rowStats = nullptr, const float* colStats = nullptr,
                         const fp16_t* bias = nullptr, int32_t* ws = nullptr, long long ws_bytes = 0) {
   if (m <= 0 || n <= 0 || k <= 0) return 0;
-  // row-major operands on the 4-wave kernel (hgemm.hip HG_I8_*, one wave per SIMD, 128 x 128 per wave) only when
-  // forced (cigemm_set_tile(4)): bit-identical, but 163 vs 142 us at 4096 x 4096 x 11008 and 82 vs 60 us at 4096^3
-  // against igemm_256's 8 waves (tools/int8_4wave_ab.py, profiles/lab/r03_int8_4wave_ab.txt) -- the int8 MFMA
-  // stream wants the second wave per SIMD that the bf16 one does not
+  // Row-major operands with the fused dequant on the 4-wave kernel (hgemm.hip HG_I8_DEQ, one wave per SIMD, 128 x 128
+  // per wave, the three-barrier schedule) wherever its grid is one mostly full round (>= 192 tiles of 256 x 256):
+  // bit-identical to igemm_256's 8 waves and faster since round 4 -- 127.3-129.3 vs 138.4-141.3 us at
+  // 4096 x 4096 x 11008, 54.4-55.2 vs 58.8-59.6 us at 4096^3 (tools/hgemm_variant_ab.py,
+  // profiles/lab/r04_hgemm_variants.txt).  Round 3 measured it slower (163 vs 142 us): its epilogue loaded the column
+  // statistics and bias once per accumulator (256 dependent loads per lane, ~34 us of fixed cost per launch); they
+  // are loaded once per lane now.  Smaller grids keep igemm_256's exact split-K; the int32 form stays there too.
   if constexpr (AF == ROW && BF == ROW && (EPI == EPI_F16_ROW_DEQUANT || EPI == EPI_I32_ROW)) {
-    if (g_igemm_tile == 4 && hgemm_tiles(m, n) >= 1) {
+    if (g_igemm_tile == 4 || (g_igemm_tile == 0 && EPI == EPI_F16_ROW_DEQUANT && hgemm_tiles(m, n) >= 192)) {
       const int rc = igemm_4wave(m, n, k, A, lda, B, ldb, C, ldc, EPI == EPI_F16_ROW_DEQUANT, rowStats, colStats, bias);
       if (rc != 1) return rc == 0 ? 0 : 1;
     }
@@ -812,7 +815,8 @@ void cextractOutliers_ampere(char* A, int* idx, char* out, int idx_size, int row
   BNB_LAUNCH_CHECK("extract_outliers");
 }
 
-// [additive, testing] 0 = auto, 128 = force the 128x128 int8 GEMM kernel
+// [additive, testing] 0 = auto, 128 = force the 128x128 int8 GEMM kernel, 4 = the 4-wave kernel (row-major operands),
+// 8 = the 8-wave igemm_256
 void cigemm_set_tile(int tile) { g_igemm_tile = tile; }
 
 }  // extern "C"

@@ -731,19 +731,23 @@ GEMM_4BIT_DEQUANT_MIN_FEATURES = 1024
 # nested statistics the Python side calls its one-launch entry point directly.
 GEMM_4BIT_FEW_TOKENS = 64
 # Between GEMM_4BIT_FEW_TOKENS and this many rows, weights at least twice as wide (out features) as deep (in
-# features) also take the library pair: its 64-row tiles cover the wide output where the fused kernel's 256-wide
-# tile grid needs split-K (tools/smallm_sweep.py, profiles/lab/r02_routing.txt, graph replay, us fused vs library:
+# features) also take the dequantise + GEMM pair (round 4: k_hgemm split-K; round 2: the library GEMM): its full-K
+# GEMM covers the wide output where the fused kernel's 256-wide tile grid needs split-K (tools/smallm_sweep.py, profiles/lab/r02_routing.txt, graph replay, us fused vs library:
 # 11008 x 4096 at 64 / 128 / 256 rows 53.8 / 58.8 / 67.5 vs 45.1 / 50.6 / 65.1; 4096 x 4096 27.0 / 31.8 / 35.0 vs
 # 29.5 / 36.0 / 34.0; 4096 x 11008 36.3 / 38.8 / 48.9 vs 52.7 / 71.2 / 64.4).
 GEMM_4BIT_WIDE_MAX_ROWS = 256
-# 2..GEMM_4BIT_GEMV_TOKENS activation rows run the multi-row GEMV (gemv4bit_tok.hip: every weight byte looked up
-# once and dotted with each row, whole K per workgroup, one launch, rows bit-identical to gemv_4bit on each row).
+# 2..GEMM_4BIT_GEMV_TOKENS activation rows: where the C side's rule takes the shape (cgemm_4bit_fewtok_takes; round 3,
+# measured faster), the whole-K MFMA few-token kernel (gemm4bit_fewtok.hip); elsewhere the multi-row GEMV
+# (gemv4bit_tok.hip: every weight byte looked up once and dotted with each row, whole K per workgroup, one launch,
+# rows bit-identical to gemv_4bit on each row).  Batch invariance is therefore given up by default: on the MFMA kernel
+# a row of a 2..4-row batch is within the GEMV tolerance of gemv_4bit on that row, not bit-identical to it (both are
+# deterministic run to run; tests/test_matmul4bit_gpu.py::test_fewtok_default_rows_close_to_gemv_and_deterministic).
+# set_fewtok_mode(1) restores the bit-identical multi-row GEMV.
 GEMM_4BIT_GEMV_TOKENS = 4
 
 # The large-prefill GEMM after the dequantise is the hand-written k_hgemm (hgemm.hip, chgemm_tn_*: 256 x 256 tiles,
-# 4 waves x 128 x 128 on v_mfma_f32_16x16x32) wherever its tile grid fills the chip (at least HGEMM_MIN_TILES tiles
-# of 256 x 256); smaller grids keep the library GEMM (torch.matmul).  4096 x 4096 x 11008: 229-231 us (1.60 PFLOP/s)
-# against rocBLAS's 215-217 us on the same box (profiles/lab/r03_hgemm_variants.txt).
+# 4 waves x 128 x 128 on v_mfma_f32_16x16x32) on every shape it takes (_hgemm_fits); tile grids below HGEMM_MIN_TILES
+# tiles of 256 x 256 run it split-K over the GEMM workspace (the C side's rule, hgemm.hip hgemm_split).
 HGEMM_MIN_TILES = 192
 
 # Routing is deterministic by default: the static rule above picks the kernel from the shape alone, so every process
@@ -804,16 +808,38 @@ def _load_route_plan():
 
 
 def _save_route_plan():
+    """Merge this process's measured routes into the plan file: under an exclusive lock on `<plan>.lock`, re-read the
+    file, add the entries it does not hold yet (a route another rank measured first wins, so every process that reads
+    the file afterwards routes the same way), adopt its entries here too, and replace it atomically.  A plan that
+    cannot be written (missing directory, permissions) is a warning, never an error of the GEMM call."""
     path = _plan_path()
     if not path:
         return
+    import fcntl
     import json
     import tempfile
-    d = os.path.dirname(os.path.abspath(path))
-    fd, tmp = tempfile.mkstemp(dir=d, prefix=".route_plan")
-    with os.fdopen(fd, "w") as f:
-        json.dump(export_routes(), f, indent=1)
-    os.replace(tmp, path)   # atomic: a concurrent reader sees the old or the new table, never half of one
+    import warnings
+    try:
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        with open(path + ".lock", "a") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            try:
+                if os.path.exists(path):
+                    with open(path) as f:
+                        on_disk = json.load(f)
+                    for row in on_disk.get("routes", []):
+                        *key, route = row
+                        if route in GEMM_4BIT_ROUTES and len(key) == 8:
+                            _ROUTES[tuple(key)] = route     # the first measurement on disk wins
+                fd, tmp = tempfile.mkstemp(dir=d, prefix=".route_plan")
+                with os.fdopen(fd, "w") as f:
+                    json.dump(export_routes(), f, indent=1)
+                os.replace(tmp, path)   # atomic: a concurrent reader sees the old or the new table, never half of one
+            finally:
+                fcntl.flock(lk, fcntl.LOCK_UN)
+    except (OSError, ValueError) as ex:
+        warnings.warn(f"gemm_4bit route plan {path!r} not written: {ex}")
 
 
 def export_routes() -> dict:
@@ -839,27 +865,25 @@ def gemm_4bit_measured_route(A: Tensor, state: QuantState, absmax: Optional[Tens
     return _ROUTES.get(_route_key(A.reshape(-1, state.shape[1]), state, absmax))
 
 
-HGEMM_SPLIT_MIN_K = 16384
-
-
 def _hgemm_fits(rows: int, N: int, K: int) -> bool:
-    """chgemm_tn's own rule (k % 64, 32-bit lane offsets) plus where it is the static choice: a tile grid that fills
-    the chip, or a long K on a smaller grid (split-K over the GEMM workspace, chgemm_tn_ws_*).  Measured
-    (tools/route_probe3.py, profiles/lab/r03_routes.txt): 4096 x 1024 x 28672 (the 70B down-projection shard) 207 us
-    split-K against 342 (torch.matmul) and 228 (rocBLAS searched); below K = 16384 the small grids stay on
-    torch.matmul (4096 x 1024 x 8192 74.8 vs 76.7 us, 2048 x 3584 x 8192 114.7 vs 152.9)."""
-    tiles = ((rows + 255) // 256) * ((N + 255) // 256)
-    return (K % 64 == 0 and (tiles >= HGEMM_MIN_TILES or (K >= HGEMM_SPLIT_MIN_K and N % 4 == 0))
+    """chgemm_tn's own rule: k % 64 == 0 and every 32-bit lane offset (row * K * 2 bytes) below 4 GiB.  Round 4: the
+    hand-written GEMM is the static choice wherever it fits -- full grids unsplit, grids below 192 tiles of 256 x 256
+    as split-K over the GEMM workspace (chgemm_tn_ws_*; N % 4 == 0, else unsplit); the library GEMM only where this
+    rule fails.  Round-3 measurements (tools/route_probe3.py, profiles/lab/r03_routes.txt): 4096 x 1024 x 28672 (the
+    70B down-projection shard) 207 us split-K against 342 (torch.matmul) and 228 (rocBLAS searched); 4096 x 1024 x 8192
+    76.7 vs 74.8 us on torch.matmul."""
+    return (K % 64 == 0 and rows >= 1 and N >= 1
             and (rows - 1) * K * 2 + 2 * K <= 0xFFFFFFFF and (N - 1) * K * 2 + 2 * K <= 0xFFFFFFFF)
 
 
 def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
-    """The deterministic route of a (rows, N, K) product: "hgemm" / "library" for large prefill, else "fused" (the
-    few-token kernels and the multi-row GEMV are picked inside the fused branch)."""
-    if rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES:
+    """The deterministic route of a (rows, N, K) product: "hgemm" (dequantise + the hand-written k_hgemm) for large
+    prefill and for 65..256 rows of a weight at least twice as wide as deep, else "fused" (the few-token kernels and
+    the multi-row GEMV are picked inside the fused branch).  "library" only for a shape k_hgemm does not take
+    (_hgemm_fits: k % 64, 32-bit offsets) -- never for a shape gemm_4bit supports with the default alignment."""
+    if (rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES) or (
+            GEMM_4BIT_FEW_TOKENS < rows <= GEMM_4BIT_WIDE_MAX_ROWS and N >= 2 * K):
         return "hgemm" if _hgemm_fits(rows, N, K) else "library"
-    if GEMM_4BIT_FEW_TOKENS < rows <= GEMM_4BIT_WIDE_MAX_ROWS and N >= 2 * K:
-        return "library"
     return "fused"
 
 
@@ -917,16 +941,13 @@ def _dequant_workspace(device, dtype, numel: int) -> Tensor:
     return ws[:numel]
 
 
-@functools.lru_cache(maxsize=4096)
-def _fewtok_takes_cached(mode: int, n: int, rows: int, k: int, blocksize: int) -> bool:
-    return bool(lib.cgemm_4bit_fewtok_takes(ct.c_int32(n), ct.c_int32(rows), ct.c_int32(k), ct.c_int32(blocksize)))
-
-
 def _fewtok_takes(n: int, rows: int, k: int, blocksize: int) -> bool:
     """Whether the C side runs the whole-K few-token kernel (gemm4bit_fewtok.hip) for this shape; 2..4 rows then go
     there instead of the multi-row GEMV (measured faster wherever its rule takes the shape, profiles/lab/r03_fewtok32.txt).
-    Cached per shape and the kernel's test knob (cgemm_4bit_set_fewtok_mode, mirrored in _FEWTOK_MODE)."""
-    return _fewtok_takes_cached(_FEWTOK_MODE[0], n, rows, k, blocksize)
+    Asked on every call (one cheap ctypes call, 2..4-row products only): the C answer applies the same conditions as the
+    launch, including every A/B knob (fewtok mode, the older few-token kernels, the split-K geometry), so no cached
+    answer can go stale when a knob changes."""
+    return bool(lib.cgemm_4bit_fewtok_takes(ct.c_int32(n), ct.c_int32(rows), ct.c_int32(k), ct.c_int32(blocksize)))
 
 
 _FEWTOK_MODE = [0]
@@ -1005,6 +1026,10 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         measured = gemm_4bit_measured_route(A2, state, absmax)   # a table handed over by import_routes / the plan file
         if measured is not None:
             route = measured
+    if route == "hgemm" and not _hgemm_fits(rows, N, K):
+        # a measured / imported route covers a quarter-octave of row counts: near the 32-bit offset limit the
+        # hand-written GEMM may not take these rows -- use the library GEMM instead of failing
+        route = "library"
     library = route in ("library", "library_tn", "hgemm")
     if (not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and not _fewtok_takes(N, rows, K, state.blocksize)
             and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events)):

@@ -217,3 +217,32 @@ def test_matmul_4bit_single_row_routing(dev):
         else:
             with pytest.raises(ValueError):
                 bnb.matmul_4bit(torch.randn(1, n_out, device=dev, dtype=torch.bfloat16), q, st)
+
+
+def test_matmul_4bit_row_count_and_orientation_square_weight(dev):
+    """matmul_4bit keeps the reference's routing (ref:autograd/_functions.py:557-577): one activation row without grad
+    goes to gemv_4bit(A, B.t()), which computes A @ W^T whichever orientation B is handed in; two or more rows go to
+    MatMul4Bit.  Pinned on a SQUARE weight, where both orientations are accepted:
+      * B = W_packed.t() (what Linear4bit passes): 1 row and 2 rows both compute A @ W^T -- batch-size independent;
+      * B = W_packed untransposed: 1 row computes A @ W^T (the GEMV), 2 rows A @ W (MatMul4Bit dequantises B and
+        applies linear(A, W.t())) -- the reference's own orientation quirk, kept for parity and documented here."""
+    import python_src_quants.functional as F
+    from python_src_quants.autograd._functions import matmul_4bit
+    torch.manual_seed(21)
+    K = 256
+    W = (torch.randn(K, K, device=dev) * 0.05).to(torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4")
+    Wd = F.dequantize_4bit(q, st).float()
+    X = torch.randn(2, K, device=dev, dtype=torch.bfloat16)
+
+    def close(got, exp):
+        rms = exp.pow(2).mean().sqrt().item()
+        return (got.float() - exp).abs().max().item() <= 2e-2 * rms + 2e-2 * exp.abs().max().item()
+    WT, WN = X.float() @ Wd.t(), X.float() @ Wd
+    assert not close(WN, WT)                                          # the two orientations differ on this weight
+    one_t = matmul_4bit(X[:1], q.t(), quant_state=st)
+    two_t = matmul_4bit(X, q.t(), quant_state=st)
+    assert close(one_t.reshape(1, K), WT[:1]) and close(two_t, WT)
+    one_n = matmul_4bit(X[:1], q, quant_state=st)
+    two_n = matmul_4bit(X, q, quant_state=st)
+    assert close(one_n.reshape(1, K), WT[:1]) and close(two_n, WN)

@@ -150,8 +150,9 @@ def test_gemm_4bit_hgemm_route_vs_oracle(dev, dtype, nested):
 
 @pytest.mark.parametrize("mnk", [(4096, 4096, 4096), (700, 900, 1024), (256, 512, 128)])
 def test_int8_on_the_4wave_kernel_is_bit_identical(dev, mnk):
-    """The same kernel body for int8 (HG_I8_DEQ, forced by cigemm_set_tile(4)): the fused mm_dequant bits equal the
-    default int8 kernels' (igemm_256 / the 128-tile kernel) -- both exact int32 sums then the same dequant.  The int32
+    """The same kernel body for int8 (HG_I8_DEQ, forced by cigemm_set_tile(4); the default for full grids since round
+    4): the fused mm_dequant bits equal the 8-wave igemm_256's (cigemm_set_tile(8)) / the 128-tile kernel's and the
+    default route's -- all exact int32 sums then the same dequant.  The int32
     product itself (igemm_rowmajor) stays on the default kernels under the knob; checked exact here."""
     F = _F()
     m, n, k = mnk
@@ -163,14 +164,14 @@ def test_int8_on_the_4wave_kernel_is_bit_identical(dev, mnk):
     bias = torch.randn(n, device=dev, generator=g).half()
     outs = {}
     try:
-        for tile in (4, 0):
+        for tile in (4, 8, 0):
             F.lib.cigemm_set_tile(tile)
             outs[tile] = (F.igemmlt_dequant(A, B, rs, cs, bias=bias), F.igemm_rowmajor(A, B))
     finally:
         F.lib.cigemm_set_tile(0)
     torch.cuda.synchronize()
-    assert torch.equal(outs[4][1], outs[0][1])
-    assert torch.equal(outs[4][0], outs[0][0])
+    assert torch.equal(outs[4][1], outs[8][1]) and torch.equal(outs[0][1], outs[8][1])
+    assert torch.equal(outs[4][0], outs[8][0]) and torch.equal(outs[0][0], outs[8][0])
     exact = (A.double() @ B.double().t())
     assert torch.equal(outs[4][1].double(), exact)
 
@@ -240,7 +241,7 @@ def test_hgemm_schedule_variants_bit_identical(dev, mnk):
     cs = torch.rand(n, device=dev, generator=g) * 2 + 0.5
     bias = torch.randn(n, device=dev, generator=g).half()
     res = {}
-    for tile, v in ((0, 0), (4, 0), (4, 1)):
+    for tile, v in ((8, 0), (4, 0), (4, 1)):
         F.lib.cigemm_set_tile(tile)
         prev = F.lib.chgemm_set_variant(v)
         try:
@@ -249,4 +250,4 @@ def test_hgemm_schedule_variants_bit_identical(dev, mnk):
         finally:
             F.lib.chgemm_set_variant(prev)
             F.lib.cigemm_set_tile(0)
-    assert torch.equal(res[(0, 0)], res[(4, 0)]) and torch.equal(res[(0, 0)], res[(4, 1)])
+    assert torch.equal(res[(8, 0)], res[(4, 0)]) and torch.equal(res[(8, 0)], res[(4, 1)])

@@ -879,3 +879,26 @@ def test_fewtok32_kernel_vs_oracle(dev, dtype, nested, qt, bs, mnk):
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
     frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
     assert frac == 0.0, err
+
+
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("rows", [2, 3, 4])
+@pytest.mark.parametrize("shape", [(11008, 4096), (4096, 4096), (4096, 11008)])
+def test_fewtok_default_rows_close_to_gemv_and_deterministic(dev, nested, rows, shape):
+    """The DEFAULT route of 2..4 activation rows (round 3: the whole-K MFMA few-token kernel wherever
+    cgemm_4bit_fewtok_takes says so, else the multi-row GEMV): each row within the GEMV tolerance of gemv_4bit on that
+    row alone (|d| <= 2e-2 * rms + 2e-2 * |ref|; bit-identity is given up on the MFMA kernel), and the same bits on a
+    second call (deterministic)."""
+    F = _F()
+    N, K = shape
+    torch.manual_seed(N + 3 * K + rows)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(rows, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    Y = F.gemm_4bit(X, q, st)
+    Y2 = F.gemm_4bit(X, q, st)
+    assert torch.equal(Y, Y2)
+    for t in range(rows):
+        y = F.gemv_4bit(X[t:t + 1], q.t(), state=st).reshape(-1).float()
+        rms = y.pow(2).mean().sqrt().item()
+        assert torch.all((Y[t].float() - y).abs() <= 2e-2 * rms + 2e-2 * y.abs()), f"row {t}"

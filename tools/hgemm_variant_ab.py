@@ -1,6 +1,6 @@
 """A/B of the k_hgemm schedules (chgemm_set_variant 0 = default, 1 = the alternative arm) on the library's own entry
 points, interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24): bf16 chgemm_tn at the metric shape
-and the int8 igemmlt + dequant on the 4-wave body (cigemm_set_tile(4)) against the 8-wave igemm_256 (tile 0).  Outputs
+and the int8 igemmlt + dequant on the 4-wave body (cigemm_set_tile(4)) against the 8-wave igemm_256 (tile 8).  Outputs
 of every arm are compared bit for bit.  Usage: python tools/hgemm_variant_ab.py [rounds]"""
 import ctypes as ct
 import os
@@ -46,7 +46,7 @@ def main():
         O8 = torch.empty(m, n, device=dev, dtype=torch.float16)
         i8 = lambda A8=A8, B8=B8, rs=rs, cs=cs, bias=bias, O8=O8: F.igemmlt_dequant(A8, B8, rs, cs, bias=bias, out=O8)  # noqa
         arms[(m, n, k)] = [("bf16 v0", 0, None, bf16, Y), ("bf16 v1", 1, None, bf16, Y),
-                           ("i8 4w v0", 0, 4, i8, O8), ("i8 4w v1", 1, 4, i8, O8), ("i8 8w", 0, 0, i8, O8)]
+                           ("i8 4w v0", 0, 4, i8, O8), ("i8 4w v1", 1, 4, i8, O8), ("i8 8w", 0, 8, i8, O8)]
     # clock ramp
     t_end = time.perf_counter() + 0.5
     while time.perf_counter() < t_end:

@@ -16,7 +16,8 @@ SHAPES = [  # (rows, out features, in features)
     (2048, 1024, 8192), (2048, 3584, 8192), (2048, 1024, 28672),
     (4096, 2048, 8192), (4096, 2048, 28672), (4096, 7168, 8192),                         # 70B 4-way shards
     (2048, 4096, 4096), (2048, 11008, 4096), (2048, 4096, 11008),                         # 7B at 2048 tokens
-    (4096, 4096, 11008), (4096, 11008, 4096), (1024, 4096, 11008), (512, 11008, 4096), (256, 11008, 4096),
+    (4096, 4096, 11008), (4096, 11008, 4096), (1024, 4096, 11008), (512, 11008, 4096), (256, 11008, 4096), (128, 11008, 4096), (96, 11008, 4096),
+    (200, 8192, 2048),
 ]
 
 
