@@ -185,13 +185,15 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
             "frac_of_int8_peak": ops / per / 1e12 / PEAK_INT8_TOPS}
 
 
-def bench_decode_sharded(dev, world, rank, steps, warmup):
+def bench_decode_sharded(dev, world, rank, steps, warmup, gather="rccl"):
     """Decode (M = 1) on `world` GPUs: the config-2 weight (Linear4bit NF4 11008 x 4096, nested statistics) sharded by
     output feature (ColumnShardedLinear4bit.from_quantized), one step = this rank's GEMV + ONE RCCL all-gather of the
     [1, 11008/world] bf16 shard outputs + the [1, 11008] row assembled (parallel.ShardedDecode, static buffers),
     captured in one HIP graph and replayed.  At M = 1 the all-gather moves KB and is latency-bound, so
     this reports latency: us per token for the layer, max over ranks, barrier-bracketed like the main step.  Ranks
-    agree on the capture (all must succeed, else every rank replays the same step eagerly)."""
+    agree on the capture (all must succeed, else every rank replays the same step eagerly).  gather="ipc": the one-shot
+    peer-memory all-gather (parallel.IpcAllGather) in place of RCCL; the result then carries the assembled row of a
+    fixed input ("_row", for the caller's cross-check against the RCCL leg) and the polls that timed out."""
     from python_src_quants.parallel import ColumnShardedLinear4bit
     n_out, k_in = 11008, 4096
     g = torch.Generator(device=dev).manual_seed(2)
@@ -201,8 +203,9 @@ def bench_decode_sharded(dev, world, rank, steps, warmup):
     lin = ColumnShardedLinear4bit.from_quantized(q, st, world, rank)
     lin.qweight = lin.qweight.clone()
     del q
-    dec = lin.decode_step()
-    dec.set_input(torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g))
+    dec = lin.decode_step(gather=gather)
+    x_check = torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g)
+    dec.set_input(x_check)
     graph = dec.capture()
     if world > 1:
         ok = torch.tensor([1 if graph else 0], device=dev)
@@ -230,11 +233,21 @@ def bench_decode_sharded(dev, world, rank, steps, warmup):
     per = elapsed / steps
     n = n_out // world
     wbytes = n * k_in // 2 + n * k_in // BS + n * k_in // BS // 256 * 4 + 1024
-    return {"shape": [1, n_out, k_in], "n_gpus": world, "us_per_token": per * 1e6, "hip_graph": bool(graph),
-            "weight_bytes_per_rank": wbytes, "rank_weight_gbs": wbytes / per / 1e9,
-            "step": "gemv_4bit on this rank's rows" + (" + RCCL all_gather_into_tensor [1, N/g] + [1, N] assembly"
-                                                        if world > 1 else " + [1, N] copy"),
-            "note": "host wall per replayed step (barrier-bracketed, max over ranks): the latency a decode token pays"}
+    res = {"shape": [1, n_out, k_in], "n_gpus": world, "us_per_token": per * 1e6, "hip_graph": bool(graph),
+           "weight_bytes_per_rank": wbytes, "rank_weight_gbs": wbytes / per / 1e9,
+           "step": "gemv_4bit on this rank's rows" + (
+               " + one-shot peer-memory all-gather (IpcAllGather, one kernel) into the [1, N] row" if gather == "ipc"
+               else " + RCCL all_gather_into_tensor [1, N/g] + [1, N] assembly" if world > 1 else " + [1, N] copy"),
+           "note": "host wall per replayed step (barrier-bracketed, max over ranks): the latency a decode token pays"}
+    dec.set_input(x_check)
+    res["_row"] = dec().clone()
+    torch.cuda.synchronize()
+    if dec.ipc is not None:
+        res["ipc_timeouts"] = dec.ipc.timeouts()
+        res["ipc_memory"] = dec.ipc.memory_kind
+        dec.graph = None
+        dec.ipc.close()
+    return res
 
 
 def _time_graph(calls, iters):
@@ -674,6 +687,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-int8", action="store_true", help="skip the sharded int8 leg")
     ap.add_argument("--no-decode", action="store_true", help="skip the sharded decode (M = 1) leg")
+    ap.add_argument("--no-ipc", action="store_true", help="N > 1: skip the one-shot peer-memory decode all-gather leg")
     ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 ranks on one GPU")
@@ -796,6 +810,22 @@ def main():
         extras["int8_igemmlt_sharded"] = bench_int8_sharded(dev, world, rank, args.steps, args.warmup, chunks)
     if not args.no_decode:   # every rank: the sharded decode step (GEMV + all-gather) as one HIP graph
         extras["decode_sharded_config2"] = bench_decode_sharded(dev, world, rank, args.steps, args.warmup)
+        row_rccl = extras["decode_sharded_config2"].pop("_row")
+        if world > 1 and not args.no_ipc:
+            # the same step on the one-shot peer-memory all-gather; every rank takes part (exchange setup is collective)
+            try:
+                r_ipc = bench_decode_sharded(dev, world, rank, args.steps, args.warmup, gather="ipc")
+                same = torch.tensor([1 if torch.equal(r_ipc.pop("_row"), row_rccl) else 0], device=dev)
+                dist.all_reduce(same, op=dist.ReduceOp.MIN)
+                r_ipc["matches_rccl_row_bitwise"] = bool(same.item())
+                t = torch.tensor([r_ipc.get("ipc_timeouts", 0)], device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                r_ipc["ipc_timeouts"] = int(t.item())
+                if not r_ipc["matches_rccl_row_bitwise"] or r_ipc["ipc_timeouts"]:
+                    r_ipc["valid"] = False
+                extras["decode_sharded_config2_ipc"] = r_ipc
+            except Exception as ex:  # noqa: BLE001
+                extras["decode_sharded_config2_ipc"] = {"error": repr(ex)}
     if rank == 0 and world == 1 and not args.no_extras:
         extras["int8_igemmlt_metric_shape"] = bench_int8(dev, M, N, K)
         extras["int8_igemmlt_config3"] = bench_int8(dev, 4096, 4096, 4096)

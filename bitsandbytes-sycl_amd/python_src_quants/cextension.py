@@ -38,6 +38,9 @@ class BNBNativeLibrary:
         lib.cgemm_4bit_workspace_bytes.restype = ct.c_longlong
         lib.cigemmlt_workspace_bytes.restype = ct.c_longlong
         lib.chgemm_tn_workspace_bytes.restype = ct.c_longlong
+        lib.cipc_allgather_buffer_bytes.restype = ct.c_longlong
+        lib.cipc_alloc.restype = ct.c_void_p
+        lib.cipc_alloc.argtypes = [ct.c_longlong, ct.POINTER(ct.c_int)]
         for name in ("cigemmlt_turing_32", "cigemmlt_turing_8", "cigemmlt_turing_8_rowscale",
                      "cigemmlt_ampere_32", "cigemmlt_ampere_8", "cigemmlt_ampere_8_rowscale",
                      "cigemmlt_row_dequant_fp16", "cigemm_row_i32", "cigemmlt_row_dequant_ws_fp16",
@@ -48,7 +51,9 @@ class BNBNativeLibrary:
                      "cdequantize_blockwise_nested_fp16_fp4", "cdequantize_blockwise_nested_fp16_nf4",
                      "cdequantize_blockwise_nested_bf16_fp4", "cdequantize_blockwise_nested_bf16_nf4",
                      "cint8_row_quant_fp16", "cgemm_4bit_inference_nested_ws_bf16",
-                     "cgemm_4bit_inference_nested_ws_fp16", "cset_cpu_threads", "cgemm_4bit_fewtok_takes", "chgemm_tn_ws_bf16", "chgemm_tn_ws_fp16"):
+                     "cgemm_4bit_inference_nested_ws_fp16", "cset_cpu_threads", "cgemm_4bit_fewtok_takes", "chgemm_tn_ws_bf16", "chgemm_tn_ws_fp16",
+                     "cipc_handle_size", "cipc_get_handle", "cipc_open_handle", "cipc_close_handle", "callgather_ipc_16",
+                     "chgemm_set_variant"):
             getattr(lib, name).restype = ct.c_int
 
     def __getattr__(self, item):

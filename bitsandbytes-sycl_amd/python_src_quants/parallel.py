@@ -254,11 +254,12 @@ class ColumnShardedLinear4bit(torch.nn.Module):
             return F.gemv_4bit(x2, self.qweight.t(), state=self.quant_state)
         return F.gemm_4bit(x2, self.qweight, self.quant_state)
 
-    def decode_step(self, dtype=torch.bfloat16) -> ShardedDecode:
-        """A static-buffer M = 1 step (this shard's GEMV + one all-gather) for graph capture: ShardedDecode."""
+    def decode_step(self, dtype=torch.bfloat16, gather: str = "rccl") -> ShardedDecode:
+        """A static-buffer M = 1 step (this shard's GEMV + one all-gather) for graph capture: ShardedDecode.
+        gather="ipc": the one-shot peer-memory all-gather (IpcAllGather) instead of RCCL."""
         fn = lambda x, y: F.gemv_4bit(x, self.qweight.t(), out=y, state=self.quant_state)  # noqa: E731
         return ShardedDecode(fn, self.in_features, self.end - self.start, self.world, self.group, dtype,
-                             self.qweight.device)
+                             self.qweight.device, gather=gather, rank=self.rank)
 
     def forward(self, x: torch.Tensor, assemble: bool = True, chunks: int = 1) -> torch.Tensor:
         """chunks > 1 overlaps the all-gather of each token-row chunk with the next chunk's GEMM
@@ -280,6 +281,104 @@ class ColumnShardedLinear4bit(torch.nn.Module):
         return gathered_to_rows(g) if assemble else g
 
 
+class IpcAllGather:
+    """One-shot all-gather of a decode step's [1, n] shard outputs over peer memory (csrc/ipc.hip, C-ABI
+    callgather_ipc_16): SURVEY §8(e) -- at M = 1 the gather moves KB and RCCL's ~10-20 us latency would dominate a
+    decode layer, so each rank pushes its slice straight into every peer's exchange buffer (opened once through
+    hipIpc handles exchanged over the process group) with an epoch flag, waits (bounded) for all peers' flags and
+    copies the assembled [1, world * n] row out -- ONE kernel, no host synchronisation, HIP-graph capturable.  RCCL stays
+    the prefill all-gather.  The exchange buffers live as long as this object; close() frees them after a barrier.
+
+    Layout of the assembled row: rank j's columns at [j * n, (j + 1) * n) -- gathered_to_rows of the RCCL path.
+    timeouts(): polls that gave up (a peer that never pushed): 0 on a healthy step; the result of such a step is
+    not valid."""
+
+    def __init__(self, n_local: int, world: int, rank: int, group=None, device=None, dtype=torch.bfloat16):
+        import ctypes as ct
+        if dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError("IpcAllGather: bf16 / fp16 shards only")
+        if n_local % 8:
+            raise ValueError("IpcAllGather: the shard width must be a multiple of 8 (whole 16-B pieces)")
+        self.n, self.world, self.rank, self.group, self.dtype = n_local, world, rank, group, dtype
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        lib = F.lib
+        self._lib = lib
+        self._own = None
+        self._opened = []
+        self.memory_kind = None
+        # Every rank takes part in every collective below whatever happened locally (a failing rank sends None / 0),
+        # and all ranks raise together: a setup error on one rank must not leave the others waiting in a collective.
+        err = None
+        with torch.cuda.device(self.device):
+            nbytes = int(lib.cipc_allgather_buffer_bytes(world, n_local, 2))
+            kind = ct.c_int(-1)
+            ptr = lib.cipc_alloc(ct.c_longlong(nbytes), ct.byref(kind))
+            handle = None
+            if not ptr:
+                err = f"cipc_alloc: {lib.cget_last_error_message().decode()}"
+            else:
+                self._own, self.memory_kind = ptr, {2: "uncached", 1: "fine-grained", 0: "plain"}.get(kind.value)
+                h = ct.create_string_buffer(int(lib.cipc_handle_size()))
+                if lib.cipc_get_handle(ct.c_void_p(ptr), h):
+                    err = f"cipc_get_handle: {lib.cget_last_error_message().decode()}"
+                else:
+                    handle = h.raw
+            handles = [None] * world
+            dist.all_gather_object(handles, handle, group=group)
+            ptrs = []
+            if err is None and all(x is not None for x in handles):
+                for j in range(world):
+                    if j == rank:
+                        ptrs.append(ptr)
+                        continue
+                    out = ct.c_void_p()
+                    if lib.cipc_open_handle(ct.create_string_buffer(handles[j], len(handles[j])), ct.byref(out)):
+                        err = f"cipc_open_handle (rank {j}): {lib.cget_last_error_message().decode()}"
+                        break
+                    ptrs.append(out.value)
+                    self._opened.append(out.value)
+            elif err is None:
+                err = "a peer could not export its exchange buffer"
+            oks = [None] * world
+            dist.all_gather_object(oks, err is None, group=group)
+            if not all(oks):
+                self.close(barrier=False)
+                raise RuntimeError(f"IpcAllGather setup failed: {err or 'on a peer rank'}")
+            self.table = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
+            self.state = torch.zeros(4, dtype=torch.int32, device=self.device)
+            torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)         # every rank has opened every buffer before anyone pushes
+
+    def __call__(self, y: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+        """Gather y [1, n] (this rank's shard) into rows [1, world * n] on the current stream."""
+        if y.dtype != self.dtype or rows.dtype != self.dtype or y.numel() != self.n or rows.numel() != self.n * self.world:
+            raise ValueError("IpcAllGather: shard / row buffers do not match the exchange")
+        prev = F.pre_call(y.device)
+        rc = self._lib.callgather_ipc_16(F.get_ptr(self.table), self.rank, self.world, self.n, F.get_ptr(y),
+                                         F.get_ptr(rows), F.get_ptr(self.state))
+        F.post_call(prev)
+        if rc:
+            raise RuntimeError(f"IpcAllGather: callgather_ipc_16 returned {rc}")
+        return rows
+
+    def timeouts(self) -> int:
+        return int(self.state[1].item())
+
+    def close(self, barrier: bool = True):
+        """Unmap the peers' buffers and free this rank's, after every rank stopped pushing (a barrier)."""
+        if barrier:
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
+        for p in self._opened:
+            self._lib.cipc_close_handle(__import__("ctypes").c_void_p(p))
+        self._opened = []
+        if barrier:
+            dist.barrier(group=self.group)
+        if self._own:
+            self._lib.cipc_free(__import__("ctypes").c_void_p(self._own))
+            self._own = None
+
+
 class ShardedDecode:
     """The M = 1 (decode) forward of a column-sharded layer on static buffers, so one decode step -- this rank's GEMV
     into `y` [1, n], ONE all-gather of the KB-sized shard outputs into `gathered` [world, 1, n] and the [1, world*n]
@@ -289,13 +388,20 @@ class ShardedDecode:
     [1, K] into y (ColumnShardedLinear4bit.decode_step passes the GEMV); the input goes through `set_input`."""
 
     def __init__(self, local_fn: Callable, in_features: int, n_local: int, world: int, group=None,
-                 dtype=torch.bfloat16, device=None):
+                 dtype=torch.bfloat16, device=None, gather: str = "rccl", rank: Optional[int] = None):
         self.local_fn, self.world, self.group = local_fn, world, group
         self.x = torch.zeros(1, in_features, dtype=dtype, device=device)
         self.y = torch.empty(1, n_local, dtype=dtype, device=device)
         self.gathered = torch.empty(world, 1, n_local, dtype=dtype, device=device)
         self.rows = torch.empty(1, world * n_local, dtype=dtype, device=device)
         self.graph = None
+        # gather="ipc": the one-shot peer-memory all-gather (IpcAllGather) instead of RCCL's all_gather_into_tensor
+        self.ipc = None
+        if gather == "ipc":
+            r = dist.get_rank(group) if rank is None else rank
+            self.ipc = IpcAllGather(n_local, world, r, group, self.x.device, dtype)
+        elif gather != "rccl":
+            raise ValueError(f"ShardedDecode: unknown gather {gather!r}")
 
     def set_input(self, x: torch.Tensor):
         self.x.copy_(x.reshape(self.x.shape))
@@ -303,6 +409,8 @@ class ShardedDecode:
     def step(self) -> torch.Tensor:
         """One eager decode step on the static buffers; returns `rows`."""
         self.local_fn(self.x, self.y)
+        if self.ipc is not None:
+            return self.ipc(self.y, self.rows)
         gather_columns(self.y, self.world, self.group, out=self.gathered)
         if not _collective(self.world):
             self.gathered[0].copy_(self.y)
@@ -312,7 +420,7 @@ class ShardedDecode:
     def capture(self, warmup: int = 2) -> bool:
         """Capture step() into a HIP graph (side-stream warm-up first, as torch.cuda.graph requires).  Returns False
         (and leaves eager mode) when the backend cannot be captured (gloo, or a collective capture refused)."""
-        if not self.x.is_cuda or (_collective(self.world) and dist.get_backend(self.group) == "gloo"):
+        if not self.x.is_cuda or (self.ipc is None and _collective(self.world) and dist.get_backend(self.group) == "gloo"):
             return False
         s = torch.cuda.Stream(device=self.x.device)
         s.wait_stream(torch.cuda.current_stream(self.x.device))

@@ -379,6 +379,23 @@ void clion32bit_grad_bf16(bnb_bf16* g, bnb_bf16* p, float* state1, float* state2
 void cdequantize_nested_absmax_fp32(float* code2, unsigned char* q, float* absmax2, float* offset, float* out,
                                     int blocksize2, long long n);
 
+/* ---- [additive] one-shot decode all-gather over peer memory (csrc/ipc.hip; SURVEY §8(e): the M = 1 all-gather is
+ * latency-bound, "prefer a custom hipIPC one-shot all-gather").  Not in the reference (no multi-GPU code there): the
+ * RCCL all-gather stays the prefill path.  Each rank allocates one exchange buffer (cipc_alloc, bytes from
+ * cipc_allgather_buffer_bytes), exports it (cipc_get_handle), opens every peer's (cipc_open_handle), and per decode
+ * step launches callgather_ipc_16: its [n] shard is pushed into every rank's buffer with an epoch flag, the rank waits
+ * (bounded) for all flags and copies the assembled [world * n] row out.  state: device u32[4] zeroed once (epoch,
+ * timeout count, last timed-out rank + 1). ---- */
+long long cipc_allgather_buffer_bytes(int world, int n, int elem);
+void* cipc_alloc(long long bytes, int* kind);   /* kind: 2 uncached, 1 fine-grained, 0 plain device memory */
+void cipc_free(void* p);
+int cipc_handle_size(void);
+int cipc_get_handle(void* p, void* handle);
+int cipc_open_handle(const void* handle, void** out);
+int cipc_close_handle(void* p);
+int callgather_ipc_16(const unsigned long long* bufs, int rank, int world, int n, const void* y, void* rows,
+                      unsigned* state);
+
 /* ---- [additive] runtime ---- */
 void cset_stream(void* stream);            /* hipStream_t used by every launch (NULL = null stream) */
 void* cget_stream(void);

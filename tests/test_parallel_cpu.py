@@ -266,3 +266,21 @@ def test_sharded_decode_step_gloo():
     ret = mgr.dict()
     mp.spawn(_worker_decode, args=(world, port, ret), nprocs=world, join=True)
     assert all(ret[r] for r in range(world))
+
+
+def test_ipc_allgather_host_rules():
+    """Host side of the one-shot decode all-gather (no GPU needed): the exchange buffer is 512 B of flags
+    (flags[2 parities][64 ranks] u32) + 2 parities x world slots of 16-B-padded shards, the shard width must be whole
+    16-B pieces and the dtype 16-bit -- rejected before any device call."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "bitsandbytes-sycl_amd")]
+    import python_src_quants.functional as F
+    from python_src_quants.parallel import IpcAllGather
+    for world, n in ((2, 1024), (8, 1376), (8, 8), (64, 128)):
+        assert F.lib.cipc_allgather_buffer_bytes(world, n, 2) == 512 + 2 * world * ((2 * n + 15) // 16 * 16)
+    assert F.lib.cipc_handle_size() == 64
+    with pytest.raises(ValueError):
+        IpcAllGather(1001, 2, 0)
+    with pytest.raises(ValueError):
+        IpcAllGather(1024, 2, 0, dtype=torch.float32)
