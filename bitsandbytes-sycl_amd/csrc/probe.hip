@@ -81,6 +81,25 @@ __global__ void __launch_bounds__(256) k_probe_hbm_read(const pb_u32x4_t* __rest
 
 }  // namespace bnb
 
+// LDS poisoning (test support): every workgroup takes the whole 160 KiB LDS of its CU and fills it with `pattern`, so
+// the next kernel's workgroups find that pattern in any LDS byte they read before writing it (LDS is not cleared
+// between kernels).  With 0xFFFFFFFF (a NaN in fp32, bf16 and fp16) a kernel that reads a staged LDS slot before its
+// DMA landed, or a slot its loads never write, returns NaN or different bits than an unpoisoned run
+// (tests/test_lds_poison_gpu.py).  k_probe_lds_peek is the positive control: it reads LDS it never wrote.
+constexpr int PB_LDS_WORDS = 160 * 1024 / 4;
+__global__ void __launch_bounds__(256) k_probe_lds_poison(unsigned pattern) {
+  __shared__ unsigned lds[PB_LDS_WORDS];
+  for (int i = threadIdx.x; i < PB_LDS_WORDS; i += blockDim.x) lds[i] = pattern;
+  __syncthreads();
+  asm volatile("" ::"v"(lds[(threadIdx.x * 613) % PB_LDS_WORDS]));
+}
+__global__ void __launch_bounds__(256) k_probe_lds_peek(unsigned* __restrict__ out) {
+  __shared__ unsigned lds[PB_LDS_WORDS];
+  unsigned v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)&lds[threadIdx.x * 157]));
+  out[blockIdx.x * blockDim.x + threadIdx.x] = v;
+}
+
 extern "C" {
 
 // [additive, measurement] kind 0 = bf16 (v_mfma_f32_16x16x32_bf16), 1 = int8 (v_mfma_i32_16x16x64_i8), + 2 for
@@ -104,4 +123,14 @@ int cprobe_hbm_read(const void* p, long long bytes, int blocks, unsigned* sink) 
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// [additive, testing] fill the LDS of every CU with `pattern` (blocks: >= the CU count; one launch on the current stream)
+int cprobe_lds_poison(unsigned pattern, int blocks) {
+  hipLaunchKernelGGL(k_probe_lds_poison, dim3(blocks), dim3(256), 0, bnb::current_stream(), pattern);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+// [additive, testing] positive control of the poisoning: out[b * 256 + t] = an LDS word the kernel never wrote
+int cprobe_lds_peek(unsigned* out, int blocks) {
+  hipLaunchKernelGGL(k_probe_lds_peek, dim3(blocks), dim3(256), 0, bnb::current_stream(), out);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 }  // extern "C"

@@ -396,6 +396,11 @@ int cipc_close_handle(void* p);
 int callgather_ipc_16(const unsigned long long* bufs, int rank, int world, int n, const void* y, void* rows,
                       unsigned* state);
 
+/* ---- [additive, testing] LDS poisoning: fill every CU's 160 KiB LDS with `pattern` (blocks >= CU count), and the
+ * positive control that reads LDS it never wrote (csrc/probe.hip; tests/test_lds_poison_gpu.py) ---- */
+int cprobe_lds_poison(unsigned pattern, int blocks);
+int cprobe_lds_peek(unsigned* out, int blocks);
+
 /* ---- [additive] runtime ---- */
 void cset_stream(void* stream);            /* hipStream_t used by every launch (NULL = null stream) */
 void* cget_stream(void);

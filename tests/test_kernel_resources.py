@@ -51,3 +51,43 @@ def test_hgemm_m0_written_only_by_its_dma_statements(tmp_path):
             ins = line.split(";")[0].strip()
             if re.search(r"\bm0\b", ins):
                 assert re.fullmatch(r"s_mov_b32 m0, s\d+|s_add_u32 m0, m0, (0x[0-9a-f]+|\d+)", ins), (name, ins)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
+def test_hgemm_tile3_dma_count_between_waits(tmp_path):
+    """The three-barrier k_hgemm schedule (V & 8192) waits `s_waitcnt vmcnt(13)` once per k-tile, meaning "tile t+1's 16
+    LDS-DMA pieces (issued one k-tile earlier) have landed; the 13 issued since may still fly".  That count is only
+    right if exactly 16 LDS-DMA instructions -- and no other vector-memory instruction -- sit between two consecutive
+    waits of the steady-state loop, and exactly 13 of them after the previous barrier-wait pair's tile started.  Checked
+    on the ISA of every launched kind (a miscount would let fragment reads see a stage before its DMA landed)."""
+    s = tmp_path / "k.s"
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                        "-ffp-contract=off", "-I", CSRC, os.path.join(CSRC, "hgemm.hip"), "-o", str(s)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    text = s.read_text()
+    bodies = re.findall(r"^(_ZN3bnb7k_hgemmILi\dELi8208\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.S | re.M)
+    assert bodies, "no three-barrier k_hgemm kernels"
+    vmem = re.compile(r"^\s*(global_|buffer_|flat_|scratch_)")
+    for name, body in bodies:
+        lines = [ln.split(";")[0].strip() for ln in body.splitlines()]
+        waits = [i for i, ln in enumerate(lines) if ln == "s_waitcnt vmcnt(13)"]
+        assert len(waits) >= 2, (name, len(waits))
+        # the steady-state loop body: consecutive waits inside one basic-block chain (the loop) hold 16 pieces
+        counted = 0
+        for a, b in zip(waits[:-1], waits[1:]):
+            seg = lines[a + 1:b]
+            if any(re.match(r"^\.LBB", ln) for ln in seg if ln.endswith(":")) and b - a > 4000:
+                continue                                         # first / last tile forms are separate code
+            dma = sum(1 for ln in seg if ln.startswith("global_load_lds_dwordx4"))
+            other = [ln for ln in seg if vmem.match(ln) and not ln.startswith("global_load_lds_dwordx4")]
+            assert dma == 16 and not other, (name, dma, other[:3])
+            counted += 1
+            # of those 16: the previous k-tile's last 3 A pieces (after its barrier B3), then this k-tile's 13 (from its
+            # barrier B1 on) before the wait -- the 13 the wait leaves in flight
+            bars = [i for i, ln in enumerate(seg) if ln == "s_barrier"]
+            assert len(bars) >= 2, (name, bars)
+            before_b1 = sum(1 for ln in seg[:bars[1]] if ln.startswith("global_load_lds_dwordx4"))
+            after_b1 = sum(1 for ln in seg[bars[1]:] if ln.startswith("global_load_lds_dwordx4"))
+            assert (before_b1, after_b1) == (3, 13), (name, before_b1, after_b1)
+        assert counted >= 1, name

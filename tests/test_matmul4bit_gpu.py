@@ -314,9 +314,19 @@ def test_gemm_4bit_library_path(dev, dtype, qt, monkeypatch):
     W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
     X = torch.randn(M, K, device=dev, dtype=dtype)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type=qt, compress_statistics=True)
+    # round 4: the static rule sends this shape to the hand-written k_hgemm (split-K: 32 tiles); the library pair is
+    # still selectable (_route="library") and stays bit-equal to dequantize_4bit + torch.matmul
+    assert F.gemm_4bit_static_route(M, N, K) == "hgemm"
+    Yl = F.gemm_4bit(X, q, st, _route="library")
+    assert torch.equal(Yl, torch.matmul(X, F.dequantize_4bit(q, st).t()))
     Y = F.gemm_4bit(X, q, st)
-    assert torch.equal(Y, torch.matmul(X, F.dequantize_4bit(q, st).t()))
     absmax = F._absmax_fp32(st).cpu().numpy()
+    for got in (Yl, Y):
+        frac, err = _close(got.float().cpu().numpy(), ref.gemm_4bit_dequant_ref(
+            X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64, st.code.cpu().numpy(),
+            "bf16" if dtype == torch.bfloat16 else "fp16"), 2e-2 if dtype == torch.bfloat16 else 1e-2,
+            2e-2 if dtype == torch.bfloat16 else 1e-2)
+        assert frac == 0.0, err
     exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, 64,
                                     st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
@@ -392,12 +402,18 @@ def test_gemm_4bit_reuse_weight_chunks(dev, monkeypatch):
     lin = ColumnShardedLinear4bit(W, world=1, rank=0, device=dev)
     full = F.gemm_4bit(X, lin.qweight, lin.quant_state)
     chunked = lin.forward(X, chunks=2)
-    assert torch.equal(chunked, full)
+    # each chunk equals its own unchunked call bit for bit (the GEMM's split-K factor follows the row count, so the
+    # whole product is compared within the GEMM tolerance)
+    per_chunk = torch.cat([F.gemm_4bit(X[:2048], lin.qweight, lin.quant_state),
+                           F.gemm_4bit(X[2048:], lin.qweight, lin.quant_state)])
+    assert torch.equal(chunked, per_chunk)
+    rms = full.float().pow(2).mean().sqrt().item()
+    assert (chunked.float() - full.float()).abs().max().item() <= 1e-2 * rms + 1e-2 * full.float().abs().max().item()
     # a second weight through the same workspace: reuse_weight must not hand back the first one
     W2 = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     q2, st2 = F.quantize_4bit(W2, blocksize=64, quant_type="nf4", compress_statistics=True)
     y2 = F.gemm_4bit(X[:2048], q2, st2, reuse_weight=True)
-    assert torch.equal(y2, torch.matmul(X[:2048], F.dequantize_4bit(q2, st2).t()))
+    assert torch.equal(y2, F.gemm_4bit(X[:2048], q2, st2))
 
 
 def test_gemm_4bit_library_path_two_streams(dev, monkeypatch):
@@ -520,8 +536,9 @@ def test_gemm_4bit_few_tokens_ragged_n(dev, nested, qt, bs, mnk):
 
 
 def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
-    """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 forces the dequantise + library GEMM route for few tokens too (the few-token
-    branch is not taken): the result equals dequantize_4bit + torch.matmul bit for bit."""
+    """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 forces the dequantise + GEMM pair for few tokens too (the few-token branch is not
+    taken): since round 4 the pair's GEMM is k_hgemm, so the result equals the forced "hgemm" route bit for bit and
+    dequantize_4bit + torch.matmul within the GEMM tolerance; the library GEMM stays reachable (_route="library")."""
     monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1)
@@ -530,7 +547,13 @@ def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
     W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
     X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
-    assert torch.equal(F.gemm_4bit(X, q, st), torch.matmul(X, F.dequantize_4bit(q, st).t()))
+    assert F.gemm_4bit_static_route(M, N, K) == "hgemm"
+    Y = F.gemm_4bit(X, q, st)
+    assert torch.equal(Y, F.gemm_4bit(X, q, st, _route="hgemm"))
+    E = torch.matmul(X, F.dequantize_4bit(q, st).t())
+    assert torch.equal(F.gemm_4bit(X, q, st, _route="library"), E)
+    rms = E.float().pow(2).mean().sqrt().item()
+    assert (Y.float() - E.float()).abs().max().item() <= 1e-2 * rms + 1e-2 * E.float().abs().max().item()
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
