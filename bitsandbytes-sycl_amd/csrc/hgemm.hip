@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 namespace bnb {
 
@@ -155,7 +156,57 @@ static int g_hgemm_variant = 0;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
 // SPLIT (bf16 / fp16 only): the split-K form -- its epilogue stores fp32 partials only.  A separate instantiation, so
 // that each kernel has ONE epilogue reading the accumulators (two in one kernel made the allocator spill).
-template <int OP, int V = 0, bool SPLIT = false>
+// Compile-time positions of the three-barrier schedule per tile shape (MFMA index q of the k-tile after which each
+// event is issued; -1 = none).  256 x 256 (8, 8): 128 MFMAs, 16 pieces, vmcnt(13) at B3.  256 x 128 (8, 4) and
+// 128 x 256 (4, 8): 64 MFMAs, 12 pieces -- the same order scaled: the stage's B rows are read first (w1), then B1; the
+// B pieces go in while x1 is read; B2; the A pieces; B3 with the pieces issued so far left in flight; the next
+// tile's step-0 fragments one per 2 MFMAs to the end, beside the last A pieces.
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(std::integral_constant<int, N - 1>)
+template <class F, int... Q>
+__device__ __forceinline__ void hg_static_for_impl(F&& f, std::integer_sequence<int, Q...>) {
+  (f(std::integral_constant<int, Q>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void hg_static_for(F&& f) {
+  hg_static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int WI, int WJ> struct HgPlan3;
+template <> struct HgPlan3<8, 8> {
+  static constexpr int B1 = 21, B2 = 50, B3 = 88, SETB = 22, SETA = 61, VM = 13;
+  __host__ __device__ static constexpr int wread(int q) { return q < 16 && (q & 1) == 0 ? q >> 1 : -1; }
+  __host__ __device__ static constexpr int xread(int q) { return q >= 23 && q <= 44 && (q - 23) % 3 == 0 ? (q - 23) / 3 : -1; }
+  __host__ __device__ static constexpr int bpiece(int q) {
+    return q == 24 ? 0 : q == 28 ? 1 : q == 32 ? 2 : q == 36 ? 3 : q == 40 ? 4 : q == 52 ? 5 : q == 56 ? 6 : q == 60 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int apiece(int q) {
+    return q == 64 ? 0 : q == 68 ? 1 : q == 72 ? 2 : q == 76 ? 3 : q == 80 ? 4 : q == 97 ? 5 : q == 107 ? 6
+                                                                                                        : q == 117 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 31 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
+};
+template <> struct HgPlan3<8, 4> {                      // 256 x 128: 4 B pieces, 8 A pieces per wave
+  static constexpr int B1 = 9, B2 = 27, B3 = 38, SETB = 10, SETA = 22, VM = 9;
+  __host__ __device__ static constexpr int wread(int q) { return q < 8 && (q & 1) == 0 ? q >> 1 : -1; }
+  __host__ __device__ static constexpr int xread(int q) { return q >= 11 && q <= 25 && (q - 11) % 2 == 0 ? (q - 11) / 2 : -1; }
+  __host__ __device__ static constexpr int bpiece(int q) { return q == 12 ? 0 : q == 15 ? 1 : q == 18 ? 2 : q == 21 ? 3 : -1; }
+  __host__ __device__ static constexpr int apiece(int q) {
+    return q == 28 ? 0 : q == 30 ? 1 : q == 32 ? 2 : q == 34 ? 3 : q == 36 ? 4 : q == 44 ? 5 : q == 50 ? 6 : q == 56 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 23 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
+};
+template <> struct HgPlan3<4, 8> {                      // 128 x 256: 8 B pieces, 4 A pieces per wave
+  static constexpr int B1 = 17, B2 = 27, B3 = 38, SETB = 17, SETA = 33, VM = 10;
+  __host__ __device__ static constexpr int wread(int q) { return q < 16 && (q & 1) == 0 ? q >> 1 : -1; }
+  __host__ __device__ static constexpr int xread(int q) { return q >= 19 && q <= 25 && (q - 19) % 2 == 0 ? (q - 19) / 2 : -1; }
+  __host__ __device__ static constexpr int bpiece(int q) {
+    return q == 18 ? 0 : q == 20 ? 1 : q == 22 ? 2 : q == 24 ? 3 : q == 26 ? 4 : q == 28 ? 5 : q == 30 ? 6 : q == 32 ? 7 : -1;
+  }
+  __host__ __device__ static constexpr int apiece(int q) { return q == 34 ? 0 : q == 36 ? 1 : q == 46 ? 2 : q == 54 ? 3 : -1; }
+  __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 23 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
+};
+
+template <int OP, int V = 0, bool SPLIT = false, int WI = 8, int WJ = 8>
 __global__ void __launch_bounds__(HG_THREADS, 1)
 k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const void* __restrict__ Bv, long long ldb,
         void* __restrict__ Cv, long long ldc, const float* __restrict__ rowStats, const float* __restrict__ colStats,
@@ -163,9 +214,15 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   using Op = HgOpT<OP>;
   using acc_t = typename Op::acc_t;
   constexpr int E = Op::ELEM;
+  // tile shape: 2 x 2 waves of (16 WI) x (16 WJ) outputs -- 256 x 256 (8, 8), 256 x 128 (8, 4), 128 x 256 (4, 8)
+  static_assert((WI == 8 && WJ == 8) || (V & 8192) != 0, "tile shapes other than 256 x 256 run the three-barrier schedule");
+  constexpr int BM = 32 * WI, BN = 32 * WJ;
+  constexpr int TA = BM * 128, STG = TA + BN * 128;     // A tile, then B tile, per stage
+  constexpr int EPI_PITCH = 32 * WJ + 16;               // 16-bit output staging row per wave (16 B of padding)
+  constexpr int LDS_BYTES = 2 * STG > 4 * 16 * WI * EPI_PITCH ? 2 * STG : 4 * 16 * WI * EPI_PITCH;
   // split-K (ksplit > 1, small tile grids): workgroup = (tile, split s); split s multiplies k-tiles
   // [s * kchunk, min((s + 1) * kchunk, all)) and stores fp32 partials ws[s][M][N] (summed in split order afterwards)
-  const int tiles_all = ((N + HG_BN - 1) / HG_BN) * ((M + HG_BM - 1) / HG_BM);
+  const int tiles_all = ((N + BN - 1) / BN) * ((M + BM - 1) / BM);
   // (readfirstlane: the divisions by the runtime ksplit run on the VALU; their wave-uniform results must live in SGPRs,
   // not in two of the main loop's 256 VGPRs -- that spilled)
   const int wgs = xcd_remap(blockIdx.x, tiles_all * (SPLIT ? ksplit : 1));
@@ -173,12 +230,12 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   const int kt0 = split * kchunk;
   const uint8_t* A = reinterpret_cast<const uint8_t*>(Av) + (long long)kt0 * 128;
   const uint8_t* B = reinterpret_cast<const uint8_t*>(Bv) + (long long)kt0 * 128;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[HG_LDS];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // ---- tile order: XCD-contiguous ids; groups of 4 M-tiles x all N-tiles (an XCD's 32 tiles share A / B rows)
-  const int tilesN = (N + HG_BN - 1) / HG_BN, tilesM = (M + HG_BM - 1) / HG_BM;
+  const int tilesN = (N + BN - 1) / BN, tilesM = (M + BM - 1) / BM;
   const int wg = SPLIT ? __builtin_amdgcn_readfirstlane(wgs / ksplit) : wgs;
   constexpr int GROUP = 4;
   const int group_span = GROUP * tilesN;
@@ -186,28 +243,34 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   const int gsize = min(tilesM - first_m, GROUP);
   const int tm = first_m + (wg % group_span) % gsize;
   const int tn = (wg % group_span) / gsize;
-  const int m0 = tm * HG_BM, n0 = tn * HG_BN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
-  // ---- DMA: wave w fills pieces p = 8w + i (tile rows 8p .. 8p+7) of both operands; lane -> (row, slot)
-  // (32-bit arithmetic: the host keeps every offset below 4 GiB; 64-bit products made hipcc park each offset in a
-  // 4-register tuple)
-  uint32_t aoff[8], boff[8];
+  // ---- DMA: wave w fills A pieces p = WI w + i and B pieces p = WJ w + i (tile rows 8p .. 8p+7); lane -> (row,
+  // slot).  (32-bit arithmetic: the host keeps every offset below 4 GiB; 64-bit products made hipcc park each offset
+  // in a 4-register tuple)
+  uint32_t aoff[WI], boff[WJ];
   const uint32_t lda2 = (uint32_t)lda * E, ldb2 = (uint32_t)ldb * E;   // row strides in bytes
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = 8 * (8 * wave + i) + (lane >> 3);
+  for (int i = 0; i < WI; ++i) {
+    const int row = 8 * (WI * wave + i) + (lane >> 3);
     const uint32_t slot = (uint32_t)((lane & 7) ^ ((row >> 1) & 7));
     aoff[i] = (uint32_t)min(m0 + row, M - 1) * lda2 + 16u * slot;
+  }
+#pragma unroll
+  for (int i = 0; i < WJ; ++i) {
+    const int row = 8 * (WJ * wave + i) + (lane >> 3);
+    const uint32_t slot = (uint32_t)((lane & 7) ^ ((row >> 1) & 7));
     boff[i] = (uint32_t)min(n0 + row, N - 1) * ldb2 + 16u * slot;
   }
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem) + wave * 8192;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
+  const uint32_t ldsA0 = lds_base + wave * WI * 1024, ldsB0 = lds_base + TA + wave * WJ * 1024;
   auto dma_a = [&](int kt, int st, int i) {
-    if constexpr ((V & 16) != 0) glds16_sv_m0(A + (long long)kt * 128, aoff[i], lds0 + st * HG_STAGE + i * 1024);
-    else glds16_sv(A + (long long)kt * 128, aoff[i], lds0 + st * HG_STAGE + i * 1024);
+    if constexpr ((V & 16) != 0) glds16_sv_m0(A + (long long)kt * 128, aoff[i], ldsA0 + st * STG + i * 1024);
+    else glds16_sv(A + (long long)kt * 128, aoff[i], ldsA0 + st * STG + i * 1024);
   };
   auto dma_b = [&](int kt, int st, int i) {
-    if constexpr ((V & 16) != 0) glds16_sv_m0(B + (long long)kt * 128, boff[i], lds0 + st * HG_STAGE + HG_TILE + i * 1024);
-    else glds16_sv(B + (long long)kt * 128, boff[i], lds0 + st * HG_STAGE + HG_TILE + i * 1024);
+    if constexpr ((V & 16) != 0) glds16_sv_m0(B + (long long)kt * 128, boff[i], ldsB0 + st * STG + i * 1024);
+    else glds16_sv(B + (long long)kt * 128, boff[i], ldsB0 + st * STG + i * 1024);
   };
 
   // ---- fragments: MFMA A operand = B rows (n), MFMA B operand = A rows (m), so D[n][m] and a lane's 4 results
@@ -215,16 +278,17 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   // fragment index, so each operand needs one lane offset per k32 step.
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fg = lane >> 4, key = (fr >> 1) & 7;
-  const int xo0 = (128 * wm + fr) * 128 + ((fg ^ key) << 4), xo1 = (128 * wm + fr) * 128 + (((4 + fg) ^ key) << 4);
-  const int wo0 = HG_TILE + (128 * wn + fr) * 128 + ((fg ^ key) << 4);
-  const int wo1 = HG_TILE + (128 * wn + fr) * 128 + (((4 + fg) ^ key) << 4);
+  const int xo0 = (16 * WI * wm + fr) * 128 + ((fg ^ key) << 4);
+  const int xo1 = (16 * WI * wm + fr) * 128 + (((4 + fg) ^ key) << 4);
+  const int wo0 = TA + (16 * WJ * wn + fr) * 128 + ((fg ^ key) << 4);
+  const int wo1 = TA + (16 * WJ * wn + fr) * 128 + (((4 + fg) ^ key) << 4);
   using frag_t = hg_u32x4_t;
   auto rd = [&](int st, int off, int f) -> frag_t {
-    return *reinterpret_cast<const frag_t*>(smem + st * HG_STAGE + off + f * 2048);
+    return *reinterpret_cast<const frag_t*>(smem + st * STG + off + f * 2048);
   };
 
-  acc_t acc[8][8];
-  frag_t w0[8], x0[8], w1[8], x1[8];
+  acc_t acc[WJ][WI];
+  frag_t w0[WJ], x0[WI], w1[WJ], x1[WI];
   const int nk = min(kchunk, K * E / 128 - kt0);   // k-tiles of 128 bytes in this split (>= 1 by the host rule)
 
   // V & 512 (lab): register-staged copies instead of LDS-DMA -- ordinary 16-B global loads into 16 staging registers
@@ -241,7 +305,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   };
   auto rs_write = [&](int st, int q) {
     if constexpr (RS)
-      *reinterpret_cast<frag_t*>(smem + st * HG_STAGE + (q < 8 ? 0 : HG_TILE) + wave * 8192 + (q & 7) * 1024 +
+      *reinterpret_cast<frag_t*>(smem + st * STG + (q < 8 ? 0 : TA) + wave * 8192 + (q & 7) * 1024 +
                                  16 * lane) = sg[q];
   };
 
@@ -292,14 +356,14 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       if constexpr ((V & 1024) != 0) return;            // lab ablation: no copies at all (timing only)
       if constexpr ((V & 4096) != 0) {                   // M0 chained from piece to piece (pieces issued in order)
         if (q < 7) glds16_chain<1024>(A + (long long)kn * 128, aoff[q]);
-        else if (q == 7) glds16_chain<HG_TILE - 7 * 1024>(A + (long long)kn * 128, aoff[7]);
+        else if (q == 7) glds16_chain<TA - 7 * 1024>(A + (long long)kn * 128, aoff[7]);
         else glds16_chain<1024>(B + (long long)kn * 128, boff[q - 8]);
         return;
       }
       if (q < 8) dma_a(kn, st, q);
       else dma_b(kn, st, q - 8);
     };
-    if constexpr (!L && (V & 4096) != 0) hg_set_m0(lds0 + st * HG_STAGE);
+    if constexpr (!L && (V & 4096) != 0) hg_set_m0(ldsA0 + st * STG);
     // fragment q of the next step 0, in the order its MFMAs need them (w0[0], x0[0..7], w0[1..7]) unless V & 4 == 0
     auto rdn = [&](int q) {
       if constexpr ((V & 4) != 0) {
@@ -368,7 +432,8 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     }
   };
 
-  // V & 8192: the operand-split schedule, three barriers per k-tile (128 MFMAs), MFMA index q:
+  // V & 8192: the operand-split schedule, three barriers per k-tile.  For the 256 x 256 tile (WI = WJ = 8, 128 MFMAs per
+  // k-tile), MFMA index q:
   //   q 0..14   this wave reads step 1's B fragments (w1) of the stage, one per 2 MFMAs;
   //   q 21      lgkmcnt(0) + barrier B1: every wave is done with the stage's B rows, so tile t+2's B pieces go into
   //             them from q 24 on (5 before B2, 3 after), while this wave reads step 1's A fragments (x1, q 23..44);
@@ -377,59 +442,47 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   //             earlier, has landed for this wave) + barrier B3 (... for every wave); tile t+1's step-0 fragments are
   //             read under the remaining 39 MFMAs (one per 2), beside the last 3 A pieces.
   // So a piece is issued as soon as its rows are free (from MFMA 24 instead of 64) and 13 of 16 stay in flight across
-  // the tile boundary; the fragment reads of a k-tile never share an MFMA gap with more than one DMA issue.
+  // the tile boundary; the fragment reads of a k-tile never share an MFMA gap with more than one DMA issue.  The
+  // half-width tiles (64 MFMAs per k-tile, 12 pieces) follow the same order on the HgPlan3 positions below.
+  using P3 = HgPlan3<WI, WJ>;
   auto tile3 = [&](auto first, auto last, int t) {
     constexpr bool FIRST = decltype(first)::value, L = decltype(last)::value;
+    constexpr int S = WI * WJ;                           // MFMAs per k32 step
     const int st = t & 1;
     const int kn = min(t + 2, nk - 1);
-    const uint32_t base = lds0 + st * HG_STAGE;
-    // compile-time schedule (q is a constant after the unroll)
-    constexpr int B1 = 21, B2 = 50, B3 = 88;
-    auto b_piece = [](int q) -> int {   // B piece issued after MFMA q, or -1
-      return q == 24 ? 0 : q == 28 ? 1 : q == 32 ? 2 : q == 36 ? 3 : q == 40 ? 4 : q == 52 ? 5 : q == 56 ? 6
-                                                                                                        : q == 60 ? 7 : -1;
-    };
-    auto a_piece = [](int q) -> int {   // A piece issued after MFMA q, or -1
-      return q == 64 ? 0 : q == 68 ? 1 : q == 72 ? 2 : q == 76 ? 3 : q == 80 ? 4 : q == 97 ? 5 : q == 107 ? 6
-                                                                                                         : q == 117 ? 7 : -1;
-    };
-#pragma unroll
-    for (int q = 0; q < 64; ++q) {
-      const int j = q >> 3, i = q & 7;
-      if constexpr (FIRST) acc[j][i] = Op::mma0(w0[j], x0[i]);
-      else acc[j][i] = Op::mma(w0[j], x0[i], acc[j][i]);
-      if (q < 16 && (q & 1) == 0) w1[q >> 1] = rd(st, wo1, q >> 1);
-      if (q >= 23 && q <= 44 && (q - 23) % 3 == 0) x1[(q - 23) / 3] = rd(st, xo1, (q - 23) / 3);
-      if constexpr (!L) {
-        if (q == 22) hg_set_m0(base + HG_TILE);
-        if (b_piece(q) >= 0) glds16_chain<1024>(B + (long long)kn * 128, boff[b_piece(q)]);
-        if (q == 61) hg_set_m0(base);
+    // (unrolled at compile time -- hg_static_for hands the body a constant q: with a runtime loop of 2 S iterations
+    // the unroller gave up on the 256 x 256 tile and left the accumulator and fragment arrays in scratch)
+    hg_static_for<2 * S>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int qq = q % S, j = qq / WI, i = qq % WI;
+      if constexpr (q < S) {
+        if constexpr (FIRST) acc[j][i] = Op::mma0(w0[j], x0[i]);
+        else acc[j][i] = Op::mma(w0[j], x0[i], acc[j][i]);
+      } else {
+        acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
       }
-      if (q == B1 || q == B2) {
+      if constexpr (P3::wread(q) >= 0) w1[P3::wread(q)] = rd(st, wo1, P3::wread(q));
+      if constexpr (P3::xread(q) >= 0) x1[P3::xread(q)] = rd(st, xo1, P3::xread(q));
+      if constexpr (q == P3::B1 || q == P3::B2) {
         __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0)
         if constexpr (!L) __builtin_amdgcn_s_barrier();
       }
-      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int q = 64; q < 128; ++q) {
-      const int j = (q - 64) >> 3, i = q & 7;
-      acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
       if constexpr (!L) {
-        if (a_piece(q) >= 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[a_piece(q)]);
-        if (q == B3) {
-          asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+        if constexpr (q == P3::SETB) hg_set_m0(ldsB0 + st * STG);
+        if constexpr (P3::bpiece(q) >= 0) glds16_chain<1024>(B + (long long)kn * 128, boff[P3::bpiece(q)]);
+        if constexpr (q == P3::SETA) hg_set_m0(ldsA0 + st * STG);
+        if constexpr (P3::apiece(q) >= 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[P3::apiece(q)]);
+        if constexpr (q == P3::B3) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM) : "memory");
           __builtin_amdgcn_s_barrier();
         }
-        if (q > B3 && q <= B3 + 31 && ((q - B3 - 1) & 1) == 0) {
-          const int r = (q - B3 - 1) >> 1;               // 0..15: w0[0], x0[0..7], w0[1..7] (the order of their use)
-          if (r == 0) w0[0] = rd(st ^ 1, wo0, 0);
-          else if (r <= 8) x0[r - 1] = rd(st ^ 1, xo0, r - 1);
-          else w0[r - 8] = rd(st ^ 1, wo0, r - 8);
-        }
+        constexpr int r = P3::nread(q);                  // w0[0], x0[0..WI-1], w0[1..WJ-1]: the order of their use
+        if constexpr (r == 0) w0[0] = rd(st ^ 1, wo0, 0);
+        else if constexpr (r > 0 && r <= WI) x0[r - 1] = rd(st ^ 1, xo0, r - 1);
+        else if constexpr (r > WI) w0[r - WI] = rd(st ^ 1, wo0, r - WI);
       }
-      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-    }
+      if constexpr ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    });
   };
 
   // ---- prologue: tiles 0 and 1 in flight, tile 0 landed, its step-0 fragments in registers
@@ -443,15 +496,21 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     __syncthreads();
   } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { dma_a(0, 0, i); dma_b(0, 0, i); }
+    for (int i = 0; i < WI; ++i) dma_a(0, 0, i);
+#pragma unroll
+    for (int i = 0; i < WJ; ++i) dma_b(0, 0, i);
     const int k1 = min(1, nk - 1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { dma_a(k1, 1, i); dma_b(k1, 1, i); }
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    for (int i = 0; i < WI; ++i) dma_a(k1, 1, i);
+#pragma unroll
+    for (int i = 0; i < WJ; ++i) dma_b(k1, 1, i);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(WI + WJ) : "memory");   // tile 0 landed; tile 1 in flight
     __builtin_amdgcn_s_barrier();
   }
 #pragma unroll
-  for (int f = 0; f < 8; ++f) { w0[f] = rd(0, wo0, f); x0[f] = rd(0, xo0, f); }
+  for (int f = 0; f < WJ; ++f) w0[f] = rd(0, wo0, f);
+#pragma unroll
+  for (int f = 0; f < WI; ++f) x0[f] = rd(0, xo0, f);
 
   if constexpr ((V & 8192) != 0) {
     if (nk == 1) {
@@ -481,9 +540,9 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   // (the lane's fragment row / group recomputed from mbcnt, not kept live from the prologue: at 256 VGPRs the main
   // loop has no register to spare for them)
   const int lane_e = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const int mb = m0 + 128 * wm + (lane_e & 15), nb = n0 + 128 * wn + 4 * (lane_e >> 4);
+  const int mb = m0 + 16 * WI * wm + (lane_e & 15), nb = n0 + 16 * WJ * wn + 4 * (lane_e >> 4);
   constexpr int OUT = (OP == HG_I8_I32) ? 4 : 2;
-  const bool full = (m0 + HG_BM <= M) && (n0 + HG_BN <= N) && (((ldc * OUT) & 15) == 0) &&
+  const bool full = (m0 + BM <= M) && (n0 + BN <= N) && (((ldc * OUT) & 15) == 0) &&
                     (((uintptr_t)Cv & 15) == 0);
   auto value = [&](int j, int i, int r, int n, float rs) -> float {   // HG_I8_DEQ: mm_dequant of one element
     return (float)Io<fp16_t>::to_f32(mm_dequant_value(acc[j][i][r], rs, colStats[n], bias ? (float)bias[n] : 0.0f));
@@ -499,11 +558,11 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(ws + (long long)split * M * N, (short)0,
                                                                           (int)((long long)M * N * 4), 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < WI; ++i) {
         const int m = mb + 16 * i;
         const uint32_t rowoff = (uint32_t)m * (uint32_t)N * 4u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < WJ; ++j) {
           const int n = nb + 16 * j;
           const uint32_t off = (m < M && n < N) ? rowoff + 4u * (uint32_t)n : 0x80000000u;
           // straight from the accumulator AGPRs (stores take AGPR data on gfx950): no VGPRs, no reads to schedule
@@ -516,26 +575,26 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     // 16-bit outputs of a full tile: staged through LDS so every global store writes whole 256-B row segments
     // (direct 8-B fragment stores put 16 rows x 32 B in one instruction: +4 us of epilogue per launch at 4096^2)
     __syncthreads();                                   // every wave is past its last stage read
-    uint8_t* ep = smem + wave * (128 * HG_EPI_PITCH);
+    uint8_t* ep = smem + wave * (16 * WI * EPI_PITCH);
     // HG_I8_DEQ: the lane's row / column statistics and bias loaded once, up front (the fragment registers are free
     // now): 8 row scales, 8 x 4 column scales (16-B loads: nb % 4 == 0) and 8 x 4 bias halves.  Loading them per
     // accumulator (256 dependent L1 loads per lane) cost ~24 us of fixed epilogue per launch.
-    float rsv[8];
-    f32x4_t csv[8];
-    uint2 bsv[8];
+    float rsv[WI];
+    f32x4_t csv[WJ];
+    uint2 bsv[WJ];
     if constexpr (OP == HG_I8_DEQ) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) rsv[i] = rowStats[mb + 16 * i];
+      for (int i = 0; i < WI; ++i) rsv[i] = rowStats[mb + 16 * i];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < WJ; ++j) {
         csv[j] = *reinterpret_cast<const f32x4_t*>(colStats + nb + 16 * j);
         bsv[j] = bias ? *reinterpret_cast<const uint2*>(bias + nb + 16 * j) : make_uint2(0u, 0u);
       }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < WI; ++i) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < WJ; ++j) {
         uint2 v;
         if constexpr (OP == HG_BF16 || OP == HG_FP16) {
           using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
@@ -551,25 +610,26 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
           }
           v = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
         }
-        *reinterpret_cast<uint2*>(ep + (16 * i + (lane_e & 15)) * HG_EPI_PITCH + 2 * (16 * j + 4 * (lane_e >> 4))) = v;
+        *reinterpret_cast<uint2*>(ep + (16 * i + (lane_e & 15)) * EPI_PITCH + 2 * (16 * j + 4 * (lane_e >> 4))) = v;
         __builtin_amdgcn_sched_barrier(0);   // one accumulator at a time: no VGPR burst that displaces AGPRs
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): the wave reads back only its own region
-    uint8_t* cbase = reinterpret_cast<uint8_t*>(Cv) + ((long long)(m0 + 128 * wm) * ldc + n0 + 128 * wn) * 2;
+    uint8_t* cbase = reinterpret_cast<uint8_t*>(Cv) + ((long long)(m0 + 16 * WI * wm) * ldc + n0 + 16 * WJ * wn) * 2;
+    constexpr int CPR = 2 * WJ, RPI = 64 / CPR;          // 16-B chunks per output row, rows per wave instruction
 #pragma unroll 8
-    for (int it = 0; it < 32; ++it) {
-      const int row = 4 * it + (lane_e >> 4), c16 = lane_e & 15;
-      const uint4 v = *reinterpret_cast<const uint4*>(ep + row * HG_EPI_PITCH + 16 * c16);
+    for (int it = 0; it < 16 * WI / RPI; ++it) {
+      const int row = RPI * it + lane_e / CPR, c16 = lane_e % CPR;
+      const uint4 v = *reinterpret_cast<const uint4*>(ep + row * EPI_PITCH + 16 * c16);
       *reinterpret_cast<uint4*>(cbase + (long long)row * ldc * 2 + 16 * c16) = v;
     }
   } else if (full) {
     if constexpr (OP == HG_I8_I32) {                   // int32: one 16-B store per accumulator already
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < WI; ++i) {
         const long long m = mb + 16 * i;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < WJ; ++j) {
           const int n = nb + 16 * j;
           *reinterpret_cast<hg_i32x4_t*>(reinterpret_cast<int32_t*>(Cv) + m * ldc + n) = acc[j][i];
           __builtin_amdgcn_sched_barrier(0);
@@ -578,13 +638,13 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < WI; ++i) {
       const int m = mb + 16 * i;
       const long long mc = min(m, M - 1);
       float rs = 0.f;
       if constexpr (OP == HG_I8_DEQ) rs = rowStats[mc];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < WJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = nb + 16 * j + r;
@@ -616,43 +676,71 @@ bool hgemm_fits(int m, int n, int k, long long lda, long long ldb, const void* A
 
 long long hgemm_tiles(int m, int n) { return (long long)((m + HG_BM - 1) / HG_BM) * ((n + HG_BN - 1) / HG_BN); }
 
-// Split-K for tile grids below HG_SPLIT_TILES (the 8-way-shard and mid-size prefill shapes: 4096 x 1024 is 64 tiles
-// on 256 CUs): S = the splits that bring the grid to about one workgroup per CU, each split >= HG_SPLIT_MIN_KT
-// k-tiles, at most 8; fp32 partials ws[S][m][n] summed in split order by one reduce launch (deterministic).
+// Launch plan: tile shape (256 x 256, 256 x 128 or 128 x 256) and split-K, chosen by cost in units of one 256 x 256
+// k-tile time (~1.37 us): rounds of workgroups on the CUs x k-tiles per workgroup x the shape's k-tile time (a half-width
+// tile does half the MFMAs per k-tile with relatively more copies and fragment reads: HG_HALF_KT), plus, per split, the
+// fp32 partials it writes and the reduce reads back (8 bytes per output at ~5 TB/s).  Grids of >= HG_SPLIT_TILES tiles
+// are not split.  The full 256 x 256 tile wins wherever its grid fills the chip (the metric shape: 256 tiles, one
+// round); the half-width tiles fill the chip where the 256 x 256 grid would be half empty (2048 x 4096: 128 tiles ->
+// 256 tiles of 256 x 128, no split-K) or where fewer than 256 rows waste half a 256-row tile (96..128 tokens).
+// Round 3's split rule (splits = CUs / tiles) could also overshoot the CU count by a few workgroups -- 43 tiles x 6 =
+// 258 workgroups, a second round for 2 of them (256 x 11008 x 4096: 89 us against 58 on the library GEMM,
+// tools/route_probe3.py, profiles/lab/r04_routes_before.txt).
 constexpr int HG_SPLIT_TILES = 192, HG_SPLIT_MIN_KT = 8, HG_SPLIT_MAX = 8;
-struct HgSplit {
-  int splits, kchunk;
+constexpr double HG_HALF_KT = 0.6;
+struct HgPlan {
+  int wi, wj, splits, kchunk;
 };
 int device_cu_count();   // CUs of the current device (cached; gemv4bit.hip)
-// The split count is chosen by its cost in k-tile times of one workgroup: rounds of workgroups on the CUs x the k-tiles
-// per split, plus the fp32 partials each extra split writes and the reduce reads back (8 bytes per output, at ~5 TB/s,
-// against ~1.37 us per k-tile).  Round 3's rule (splits = CUs / tiles) could overshoot the CU count by a few
-// workgroups -- 43 tiles x 6 = 258 workgroups, a second round for 2 of them (256 x 11008 x 4096: 89 us against 58 on
-// the library GEMM, tools/route_probe3.py, profiles/lab/r04_routes.txt).
-HgSplit hgemm_split(int m, int n, int k, int elem) {
-  const long long tiles = hgemm_tiles(m, n);
+static HgPlan hgemm_plan(int m, int n, int k, int elem, bool allow_split, bool full_tiles_only) {
   const int nkt = (int)((long long)k * elem / 128);
-  if (tiles >= HG_SPLIT_TILES || n % 4) return HgSplit{1, nkt};
   int cus = device_cu_count();
   if (cus <= 0) cus = 256;
   const double part_kt = (double)m * n * 8.0 / 5.0e12 / 1.37e-6;   // one split's partial traffic, in k-tile times
-  HgSplit best{1, nkt};
-  double best_cost = (double)((tiles + cus - 1) / cus) * nkt;
-  for (int s = 2; s <= HG_SPLIT_MAX; ++s) {
-    const int kchunk = (nkt + s - 1) / s;
-    if (kchunk < HG_SPLIT_MIN_KT) break;
-    const int splits = (nkt + kchunk - 1) / kchunk;
-    const double cost = (double)((tiles * splits + cus - 1) / cus) * kchunk + part_kt * splits;
+  static const int shapes[3][2] = {{8, 8}, {8, 4}, {4, 8}};
+  HgPlan best{8, 8, 1, nkt};
+  double best_cost = 1e300;
+  for (int si = 0; si < (full_tiles_only ? 1 : 3); ++si) {
+    const int wi = shapes[si][0], wj = shapes[si][1];
+    const double tkt = (wi == 8 && wj == 8) ? 1.0 : HG_HALF_KT;
+    const long long tiles = (long long)((m + 32 * wi - 1) / (32 * wi)) * ((n + 32 * wj - 1) / (32 * wj));
+    double cost = (double)((tiles + cus - 1) / cus) * nkt * tkt;
     if (cost < best_cost) {
       best_cost = cost;
-      best = HgSplit{splits, kchunk};
+      best = HgPlan{wi, wj, 1, nkt};
+    }
+    if (!allow_split || tiles >= HG_SPLIT_TILES || n % 4) continue;
+    for (int sp = 2; sp <= HG_SPLIT_MAX; ++sp) {
+      const int kchunk = (nkt + sp - 1) / sp;
+      if (kchunk < HG_SPLIT_MIN_KT) break;
+      const int splits = (nkt + kchunk - 1) / kchunk;
+      cost = (double)((tiles * splits + cus - 1) / cus) * kchunk * tkt + part_kt * splits;
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = HgPlan{wi, wj, splits, kchunk};
+      }
     }
   }
   return best;
 }
 long long hgemm_workspace_bytes(int m, int n, int k, int elem) {
-  const HgSplit sp = hgemm_split(m, n, k, elem);
-  return sp.splits > 1 ? (long long)sp.splits * m * n * (long long)sizeof(float) : 0;
+  const HgPlan pl = hgemm_plan(m, n, k, elem, true, false);
+  return pl.splits > 1 ? (long long)pl.splits * m * n * (long long)sizeof(float) : 0;
+}
+
+template <int OP, int V, int WI, int WJ>
+static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
+                               long long ldb, void* C, long long ldc, const float* rowStats, const float* colStats,
+                               const fp16_t* bias, float* ws) {
+  const unsigned tiles = (unsigned)(((m + 32 * WI - 1) / (32 * WI)) * ((n + 32 * WJ - 1) / (32 * WJ)));
+  if (pl.splits > 1) {
+    if constexpr (OP == HG_BF16 || OP == HG_FP16)
+      hipLaunchKernelGGL((k_hgemm<OP, V, true, WI, WJ>), dim3(tiles * pl.splits), dim3(HG_THREADS), 0, current_stream(), m,
+                         n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, pl.splits, pl.kchunk);
+  } else {
+    hipLaunchKernelGGL((k_hgemm<OP, V, false, WI, WJ>), dim3(tiles), dim3(HG_THREADS), 0, current_stream(), m, n, k, A,
+                       lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, pl.kchunk);
+  }
 }
 
 template <int OP>
@@ -662,34 +750,24 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   if (!hgemm_fits(m, n, k, lda, ldb, A, B, HgOpT<OP>::ELEM) || ldc < n) return 1;
   // the dequant epilogue reads 4 column scales / 4 bias halves per 16-B / 8-B load
   if (OP == HG_I8_DEQ && (((uintptr_t)colStats & 15) || ((uintptr_t)bias & 7))) return 1;
-  HgSplit sp{1, (int)((long long)k * HgOpT<OP>::ELEM / 128)};
-  if constexpr (OP == HG_BF16 || OP == HG_FP16) {
-    const HgSplit want = hgemm_split(m, n, k, HgOpT<OP>::ELEM);
-    if (want.splits > 1 && ws != nullptr && ((uintptr_t)ws & 15) == 0 &&
-        ws_bytes >= (long long)want.splits * m * n * (long long)sizeof(float))
-      sp = want;
+  constexpr bool FP = OP == HG_BF16 || OP == HG_FP16;
+  // int8 (HG_I8_DEQ) and the round-3 schedule arm (chgemm_set_variant(1)) run the 256 x 256 tile only
+  const bool full_only = !FP || g_hgemm_variant == 1;
+  HgPlan pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, FP, full_only);
+  if (pl.splits > 1 && (ws == nullptr || ((uintptr_t)ws & 15) ||
+                        ws_bytes < (long long)pl.splits * m * n * (long long)sizeof(float)))
+    pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, false, full_only);      // no (large enough) workspace: no split
+  if (g_hgemm_variant == 1) {
+    hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
+  } else if (pl.wi == 8 && pl.wj == 8) {
+    hgemm_launch_shape<OP, HG_V, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
+  } else if constexpr (FP) {
+    if (pl.wi == 8) hgemm_launch_shape<OP, HG_V, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
+    else hgemm_launch_shape<OP, HG_V, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
   }
-  if (sp.splits > 1) {
-    if constexpr (OP == HG_BF16 || OP == HG_FP16) {
-      if (g_hgemm_variant == 1)
-        hipLaunchKernelGGL((k_hgemm<OP, HG_V_ALT, true>), dim3((unsigned)(hgemm_tiles(m, n) * sp.splits)), dim3(HG_THREADS),
-                           0, current_stream(), m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sp.splits,
-                           sp.kchunk);
-      else
-        hipLaunchKernelGGL((k_hgemm<OP, HG_V, true>), dim3((unsigned)(hgemm_tiles(m, n) * sp.splits)), dim3(HG_THREADS),
-                           0, current_stream(), m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sp.splits,
-                           sp.kchunk);
-    }
-  } else if (g_hgemm_variant == 1) {
-    hipLaunchKernelGGL((k_hgemm<OP, HG_V_ALT>), dim3((unsigned)hgemm_tiles(m, n)), dim3(HG_THREADS), 0, current_stream(),
-                       m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, sp.kchunk);
-  } else {
-    hipLaunchKernelGGL((k_hgemm<OP, HG_V>), dim3((unsigned)hgemm_tiles(m, n)), dim3(HG_THREADS), 0, current_stream(), m,
-                       n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, sp.kchunk);
-  }
-  if constexpr (OP == HG_BF16 || OP == HG_FP16) {
+  if constexpr (FP) {
     using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
-    if (sp.splits > 1) launch_splitk_rows_reduce<T>(ws, sp.splits, m, n, reinterpret_cast<T*>(C), (int)ldc);
+    if (pl.splits > 1) launch_splitk_rows_reduce<T>(ws, pl.splits, m, n, reinterpret_cast<T*>(C), (int)ldc);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -736,6 +814,15 @@ int chgemm_tn_ws_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_
   return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
 }
 long long chgemm_tn_workspace_bytes(int m, int n, int k) { return bnb::hgemm_workspace_bytes(m, n, k, 2); }
+// [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k) with enough workspace: out = {WI, WJ, splits,
+// k-tiles per split}; the output tile is 32 WI x 32 WJ (256 x 256, 256 x 128 or 128 x 256)
+void chgemm_tn_plan(int m, int n, int k, int* out) {
+  const bnb::HgPlan pl = bnb::hgemm_plan(m, n, k, 2, true, bnb::g_hgemm_variant == 1);
+  out[0] = pl.wi;
+  out[1] = pl.wj;
+  out[2] = pl.splits;
+  out[3] = pl.kchunk;
+}
 // [additive, testing] k_hgemm schedule: 0 = the default, 1 = the A/B arm (HG_V_ALT); returns the previous setting
 int chgemm_set_variant(int v) {
   const int prev = bnb::g_hgemm_variant;

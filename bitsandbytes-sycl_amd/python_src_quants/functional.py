@@ -718,23 +718,21 @@ def _gemm_workspace(device, nbytes: int) -> Optional[Tensor]:
     return ws
 
 
-# From GEMM_4BIT_DEQUANT_MIN_ROWS activation rows and GEMM_4BIT_DEQUANT_MIN_FEATURES output features the
-# reference's own M > 1 algorithm -- dequantise the whole weight (our HIP kernel, HBM-bound) and run one
-# bf16/fp16 library GEMM (hipBLASLt) -- beats the fused kernel.  tools/gemm_baseline.py sweep, K = 11008
-# (fused vs dequantise + matmul, us): 4096 x 4096 331.7 vs 240.4; 2048 x 4096 189.2 vs 159.1;
-# 4096 x 1024 108.7 vs 95.0; 1024 x 4096 108.2 vs 106.2; 512 x 4096 67.6 vs 80.4; 4096 x 512 69.6 vs 70.8.
+# Prefill routing (gemm_4bit_static_route, round 4): from GEMM_4BIT_DEQUANT_MIN_ROWS activation rows always the
+# reference's own M > 1 algorithm -- dequantise the whole weight (the HIP kernel, HBM-bound) and one bf16/fp16 GEMM,
+# here the hand-written k_hgemm; below that the same pair except on deep, wide weights with few rows, where the
+# one-kernel fused NF4 GEMM wins (see the route's docstring).  GEMM_4BIT_DEQUANT_MIN_FEATURES: kept for callers and
+# tests that size a "large prefill" problem (the static rule no longer needs it).
 GEMM_4BIT_DEQUANT_MIN_ROWS = 2048
 GEMM_4BIT_DEQUANT_MIN_FEATURES = 1024
-# Up to this many activation rows the C side runs the weight-streaming kernel (gemm4bit_skinny.hip; 33..64 rows on
-# its 4-tile instance, round 2: 11008 x 4096 at 33..64 rows 43.7 -> 27.3..31.2 us against the library pair,
-# 4096 x 4096 18.4..21.0 -> 15.2..18.1 us against the tile kernels, profiles/lab/r02_fewtoken_64rows.txt); with
-# nested statistics the Python side calls its one-launch entry point directly.
+# Up to this many activation rows the C side runs the few-token kernels (gemm4bit_fewtok.hip whole-K up to 32 rows,
+# gemm4bit_skinny.hip split-K at 33..64 rows; round 2: 11008 x 4096 at 33..64 rows 43.7 -> 27.3..31.2 us against the
+# library pair, profiles/lab/r02_fewtoken_64rows.txt); with nested statistics the Python side calls its one-launch
+# entry point directly.
 GEMM_4BIT_FEW_TOKENS = 64
-# Between GEMM_4BIT_FEW_TOKENS and this many rows, weights at least twice as wide (out features) as deep (in
-# features) also take the dequantise + GEMM pair (round 4: k_hgemm split-K; round 2: the library GEMM): its full-K
-# GEMM covers the wide output where the fused kernel's 256-wide tile grid needs split-K (tools/smallm_sweep.py, profiles/lab/r02_routing.txt, graph replay, us fused vs library:
-# 11008 x 4096 at 64 / 128 / 256 rows 53.8 / 58.8 / 67.5 vs 45.1 / 50.6 / 65.1; 4096 x 4096 27.0 / 31.8 / 35.0 vs
-# 29.5 / 36.0 / 34.0; 4096 x 11008 36.3 / 38.8 / 48.9 vs 52.7 / 71.2 / 64.4).
+# (round 2's rule for 65..256 rows of wide weights; the round-4 static rule covers those rows with k_hgemm's 128-row
+# tile and split-K -- 11008 x 4096 at 96 / 128 / 256 rows 52.5 / 54.0 / 60.4 us against the library pair's 48.9 / 51.8
+# / 58.7 and the fused kernel's 62.1 / 66.2 / 74.0, profiles/lab/r04_route_sweep.txt)
 GEMM_4BIT_WIDE_MAX_ROWS = 256
 # 2..GEMM_4BIT_GEMV_TOKENS activation rows: where the C side's rule takes the shape (cgemm_4bit_fewtok_takes; round 3,
 # measured faster), the whole-K MFMA few-token kernel (gemm4bit_fewtok.hip); elsewhere the multi-row GEMV
@@ -745,9 +743,10 @@ GEMM_4BIT_WIDE_MAX_ROWS = 256
 # set_fewtok_mode(1) restores the bit-identical multi-row GEMV.
 GEMM_4BIT_GEMV_TOKENS = 4
 
-# The large-prefill GEMM after the dequantise is the hand-written k_hgemm (hgemm.hip, chgemm_tn_*: 256 x 256 tiles,
-# 4 waves x 128 x 128 on v_mfma_f32_16x16x32) on every shape it takes (_hgemm_fits); tile grids below HGEMM_MIN_TILES
-# tiles of 256 x 256 run it split-K over the GEMM workspace (the C side's rule, hgemm.hip hgemm_split).
+# The GEMM after the dequantise is the hand-written k_hgemm (hgemm.hip, chgemm_tn_*: 4 waves on v_mfma_f32_16x16x32,
+# 256 x 256 tiles -- 128 x 128 per wave -- or the half-width 256 x 128 / 128 x 256 tiles, split-K over the GEMM
+# workspace on small grids; the C side's launch plan, hgemm.hip hgemm_plan / chgemm_tn_plan) on every shape it takes
+# (_hgemm_fits).  HGEMM_MIN_TILES: the 256 x 256 grid size from which no split is considered.
 HGEMM_MIN_TILES = 192
 
 # Routing is deterministic by default: the static rule above picks the kernel from the shape alone, so every process
@@ -877,14 +876,20 @@ def _hgemm_fits(rows: int, N: int, K: int) -> bool:
 
 
 def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
-    """The deterministic route of a (rows, N, K) product: "hgemm" (dequantise + the hand-written k_hgemm) for large
-    prefill and for 65..256 rows of a weight at least twice as wide as deep, else "fused" (the few-token kernels and
-    the multi-row GEMV are picked inside the fused branch).  "library" only for a shape k_hgemm does not take
-    (_hgemm_fits: k % 64, 32-bit offsets) -- never for a shape gemm_4bit supports with the default alignment."""
-    if (rows >= GEMM_4BIT_DEQUANT_MIN_ROWS and N >= GEMM_4BIT_DEQUANT_MIN_FEATURES) or (
-            GEMM_4BIT_FEW_TOKENS < rows <= GEMM_4BIT_WIDE_MAX_ROWS and N >= 2 * K):
-        return "hgemm" if _hgemm_fits(rows, N, K) else "library"
-    return "fused"
+    """The deterministic route of a (rows, N, K) product (round 4, tools/route_sweep4.py, profiles/lab/r04_route_sweep.txt):
+      * up to GEMM_4BIT_FEW_TOKENS rows: "fused" (the few-token kernels and the multi-row GEMV, picked inside);
+      * the one-kernel fused NF4 GEMM ("fused") where the weight is deep and wide and the rows few -- K >= 8192 and
+        N >= 4096 up to 512 rows (4096 x 11008 at 96..256 rows 45-55 us vs 54-62 dequantise + k_hgemm; 8192 x 8192
+        53-96 vs 69-100), K >= 16384 at 257..1024 rows (1024 x 28672 at 1024 rows 85 vs 102): there the bf16 weight's
+        write + read costs more than the fused kernel's in-LDS dequantisation;
+      * everywhere else the dequantise + the hand-written k_hgemm ("hgemm"; 256 x 256 / 256 x 128 / 128 x 256 tiles and
+        split-K by its launch plan) -- "library" only for a shape k_hgemm does not take (k % 64, 32-bit offsets)."""
+    if rows <= GEMM_4BIT_FEW_TOKENS:
+        return "fused"
+    if rows < GEMM_4BIT_DEQUANT_MIN_ROWS:
+        if (K >= 8192 and N >= 4096 and rows <= 512) or (K >= 16384 and 256 < rows <= 1024):
+            return "fused"
+    return "hgemm" if _hgemm_fits(rows, N, K) else "library"
 
 
 def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor],

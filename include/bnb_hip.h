@@ -231,6 +231,9 @@ int chgemm_tn_ws_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb
 long long chgemm_tn_workspace_bytes(int m, int n, int k);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);
+/* [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k): out = {WI, WJ, splits, k-tiles per split};
+ * the output tile is 32 WI x 32 WJ (256 x 256, 256 x 128 or 128 x 256) */
+void chgemm_tn_plan(int m, int n, int k, int* out);
 /* [additive, measurement] measured ceilings for the bench's roofline (probe.hip): the dense MFMA rate on random operands
  * in registers (kind 0 = bf16 v_mfma_f32_16x16x32_bf16, 1 = int8 v_mfma_i32_16x16x64_i8; one wave per SIMD, 8 x iters
  * MFMAs per wave; sink >= blocks * 256 floats) and the HBM streaming read rate (bytes % 16 == 0; sink >= blocks

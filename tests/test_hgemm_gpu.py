@@ -180,18 +180,19 @@ def test_int8_on_the_4wave_kernel_is_bit_identical(dev, mnk):
 @pytest.mark.parametrize("mnk", [(4096, 1024, 8192), (4096, 1024, 28672), (1000, 1100, 4096), (512, 11008, 4096),
                                  (257, 516, 1024), (2048, 3584, 8192), (300, 260, 576)])
 def test_hgemm_split_k_against_fp32_product(dev, dtype, mnk):
-    """Small tile grids (< 192 tiles) through chgemm_tn_ws_*: split-K over fp32 partials in the caller's workspace,
-    summed in split order -- within the same fp32-product bound as the unsplit kernel (the k order differs, the
-    accumulation is fp32 either way), deterministic across calls, and the workspace query matches the split
-    (0 when the shape is not split); a too-small workspace runs the unsplit kernel."""
+    """Small tile grids through chgemm_tn_ws_*: split-K (when the launch plan picks it) over fp32 partials in the
+    caller's workspace, summed in split order -- within the same fp32-product bound as the unsplit kernel (the k order
+    differs, the accumulation is fp32 either way), deterministic across calls, and the workspace query matches the
+    plan (0 when the shape is not split); a too-small workspace runs the best unsplit plan."""
     F = _F()
     m, n, k = mnk
     g = torch.Generator(device=dev).manual_seed(m + n + k)
     X = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(dtype)
     W = (torch.rand(n, k, device=dev, generator=g) * 2 - 1).to(dtype)
     nbytes = int(F.lib.chgemm_tn_workspace_bytes(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k)))
-    tiles = ((m + 255) // 256) * ((n + 255) // 256)
-    assert (nbytes > 0) == (tiles < 192 and n % 4 == 0 and k >= 2 * 8 * 64)
+    plan = (ct.c_int * 4)()
+    F.lib.chgemm_tn_plan(m, n, k, plan)
+    assert nbytes == (plan[2] * m * n * 4 if plan[2] > 1 else 0), (tuple(plan), nbytes)
     ws = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=dev)
     fn = F.lib.chgemm_tn_ws_bf16 if dtype == torch.bfloat16 else F.lib.chgemm_tn_ws_fp16
     outs = []
@@ -251,3 +252,29 @@ def test_hgemm_schedule_variants_bit_identical(dev, mnk):
             F.lib.chgemm_set_variant(prev)
             F.lib.cigemm_set_tile(0)
     assert torch.equal(res[(8, 0)], res[(4, 0)]) and torch.equal(res[(8, 0)], res[(4, 1)])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mnk,plan", [((2048, 4096, 4096), (8, 4, 1)), ((96, 11008, 4096), (4, 8, 5)),
+                                      ((4096, 1024, 8192), (8, 4, 2)), ((128, 8192, 8192), (4, 8, 8)),
+                                      ((300, 700, 1024), None), ((2051, 1037, 640), None), ((4096, 4096, 2048), (8, 8, 1))])
+def test_hgemm_tile_shapes_against_fp32_product(dev, dtype, mnk, plan):
+    """The half-width tiles (256 x 128 and 128 x 256, picked by the launch plan for grids that a 256 x 256 tiling leaves
+    half empty or rows that waste half a 256-row tile), with and without split-K, ragged edges included: against the
+    fp32 product (the module's contract) and deterministic; chgemm_tn_plan reports the plan the shape takes."""
+    F = _F()
+    m, n, k = mnk
+    out4 = (ct.c_int * 4)()
+    F.lib.chgemm_tn_plan(m, n, k, out4)
+    if plan is not None:
+        assert tuple(out4[:3]) == plan, tuple(out4)
+    g = torch.Generator(device=dev).manual_seed(m + 7 * n + k)
+    X = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    W = (torch.rand(n, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    rc, Y = _hgemm_ws(F, X, W)
+    torch.cuda.synchronize()
+    assert rc == 0
+    _check(Y, X, W)
+    rc2, Y2 = _hgemm_ws(F, X, W)
+    torch.cuda.synchronize()
+    assert rc2 == 0 and torch.equal(Y, Y2)

@@ -55,11 +55,12 @@ def test_hgemm_m0_written_only_by_its_dma_statements(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
 def test_hgemm_tile3_dma_count_between_waits(tmp_path):
-    """The three-barrier k_hgemm schedule (V & 8192) waits `s_waitcnt vmcnt(13)` once per k-tile, meaning "tile t+1's 16
-    LDS-DMA pieces (issued one k-tile earlier) have landed; the 13 issued since may still fly".  That count is only
-    right if exactly 16 LDS-DMA instructions -- and no other vector-memory instruction -- sit between two consecutive
-    waits of the steady-state loop, and exactly 13 of them after the previous barrier-wait pair's tile started.  Checked
-    on the ISA of every launched kind (a miscount would let fragment reads see a stage before its DMA landed)."""
+    """The three-barrier k_hgemm schedule (V & 8192) waits `s_waitcnt vmcnt(VM)` once per k-tile, meaning "tile t+1's
+    LDS-DMA pieces (issued one k-tile earlier) have landed; the VM issued since may still fly" (256 x 256 tile: 16 pieces,
+    VM 13; 256 x 128: 12, 9; 128 x 256: 12, 10).  That count is only right if exactly `pieces` LDS-DMA instructions --
+    and no other vector-memory instruction -- sit between two consecutive waits of the steady-state loop, VM of them
+    after the k-tile's first barrier.  Checked on the ISA of every launched kind and tile shape (a miscount would let
+    fragment reads see a stage before its DMA landed)."""
     s = tmp_path / "k.s"
     r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
                         "-ffp-contract=off", "-I", CSRC, os.path.join(CSRC, "hgemm.hip"), "-o", str(s)],
@@ -69,9 +70,17 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
     bodies = re.findall(r"^(_ZN3bnb7k_hgemmILi\dELi8208\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.S | re.M)
     assert bodies, "no three-barrier k_hgemm kernels"
     vmem = re.compile(r"^\s*(global_|buffer_|flat_|scratch_)")
+    # per tile shape (WI, WJ): LDS-DMA pieces per k-tile and the vmcnt of barrier B3 (HgPlan3 in hgemm.hip)
+    plans = {(8, 8): (16, 13), (8, 4): (12, 9), (4, 8): (12, 10)}
+    shapes_seen = set()
     for name, body in bodies:
+        m = re.search(r"ELb[01]ELi(\d)ELi(\d)E", name)
+        assert m, name
+        shape = (int(m.group(1)), int(m.group(2)))
+        shapes_seen.add(shape)
+        pieces, vm = plans[shape]
         lines = [ln.split(";")[0].strip() for ln in body.splitlines()]
-        waits = [i for i, ln in enumerate(lines) if ln == "s_waitcnt vmcnt(13)"]
+        waits = [i for i, ln in enumerate(lines) if ln == f"s_waitcnt vmcnt({vm})"]
         assert len(waits) >= 2, (name, len(waits))
         # the steady-state loop body: consecutive waits inside one basic-block chain (the loop) hold 16 pieces
         counted = 0
@@ -81,7 +90,7 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
                 continue                                         # first / last tile forms are separate code
             dma = sum(1 for ln in seg if ln.startswith("global_load_lds_dwordx4"))
             other = [ln for ln in seg if vmem.match(ln) and not ln.startswith("global_load_lds_dwordx4")]
-            assert dma == 16 and not other, (name, dma, other[:3])
+            assert dma == pieces and not other, (name, dma, other[:3])
             counted += 1
             # of those 16: the previous k-tile's last 3 A pieces (after its barrier B3), then this k-tile's 13 (from its
             # barrier B1 on) before the wait -- the 13 the wait leaves in flight
@@ -89,5 +98,6 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
             assert len(bars) >= 2, (name, bars)
             before_b1 = sum(1 for ln in seg[:bars[1]] if ln.startswith("global_load_lds_dwordx4"))
             after_b1 = sum(1 for ln in seg[bars[1]:] if ln.startswith("global_load_lds_dwordx4"))
-            assert (before_b1, after_b1) == (3, 13), (name, before_b1, after_b1)
+            assert (before_b1, after_b1) == (pieces - vm, vm), (name, before_b1, after_b1)
         assert counted >= 1, name
+    assert shapes_seen == set(plans), shapes_seen
