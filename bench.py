@@ -732,6 +732,7 @@ def main():
     library = dequant_route(gemm_kernel_name(Mc, shard))
 
     clock = StepClock(args.steps)
+    F.reserve_stage_events(3 * (args.steps // STAGE_EVERY + 1))   # the sampled steps' stage events, made up front
 
     def step(record=False):
         # fused kernel: nested stats -> fp32 absmax once per step, shared by the chunks; library path:

@@ -964,6 +964,23 @@ def set_fewtok_mode(mode: int) -> None:
     _FEWTOK_MODE[0] = mode
 
 
+_EVENT_POOL: list = []
+
+
+def reserve_stage_events(n: int) -> None:
+    """Pre-create n timing events for the `events=` instrumentation of gemm_4bit (bench): creating them inside a timed
+    step costs host time that can leave the GPU waiting in exactly the steps that are sampled."""
+    for _ in range(n):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()                         # the HIP event itself is created at its first record
+        _EVENT_POOL.append(e)
+    torch.cuda.synchronize()
+
+
+def _stage_events(n: int) -> list:
+    return [_EVENT_POOL.pop() if _EVENT_POOL else torch.cuda.Event(enable_timing=True) for _ in range(n)]
+
+
 def _gemm_4bit_tokens(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor],
                       events: Optional[list]) -> bool:
     """2..GEMM_4BIT_GEMV_TOKENS rows through cgemm_4bit_inference_tokens_* (one launch; compressed statistics
@@ -980,7 +997,7 @@ def _gemm_4bit_tokens(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, ab
         bs2 = 0
     prev_device = pre_call(A2.device)
     is_on_gpu([A2, Bc, out, state.code] + [t for t in stats if t is not None])
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if events is not None else None
+    ev = _stage_events(2) if events is not None else None
     if ev:
         ev[0].record()
     fn = lib.cgemm_4bit_inference_tokens_bf16 if A2.dtype == torch.bfloat16 else lib.cgemm_4bit_inference_tokens_fp16
@@ -1048,7 +1065,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         offset = _offset_on(state, A.device)
         prev_device = pre_call(A.device)
         is_on_gpu([A2, Bc, out, state.absmax, s2.code, s2.absmax, offset, state.code])
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if events is not None else None
+        ev = _stage_events(2) if events is not None else None
         if ev:
             ev[0].record()
         fn = (lib.cgemm_4bit_inference_nested_ws_bf16 if A.dtype == torch.bfloat16
@@ -1068,7 +1085,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         absmax = _absmax_fp32(state)
     prev_device = pre_call(A.device)
     is_on_gpu([A2, Bc, out, state.code] + ([absmax] if absmax is not None else []))
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if events is not None else None
+    ev = _stage_events(3) if events is not None else None
     if ev:
         ev[0].record()
     if library:

@@ -235,7 +235,12 @@ def test_hgemm_schedule_variants_bit_identical(dev, mnk):
             assert rc == 0
             outs.append(Y)
         _check(outs[1], X, W)
-        assert torch.equal(outs[0], outs[1])
+        plan = (ct.c_int * 4)()
+        F.lib.chgemm_tn_plan(m, n, k, plan)
+        if (plan[0], plan[1]) == (8, 8):      # same tiles and split: same k order per accumulator, same bits
+            assert torch.equal(outs[0], outs[1])
+        else:                                 # the round-3 arm runs 256 x 256 tiles only: another split of k
+            _check(outs[0], X, W)
     A = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8, generator=g)
     B = torch.randint(-127, 128, (n, k), device=dev, dtype=torch.int8, generator=g)
     rs = torch.rand(m, device=dev, generator=g) * 2 + 0.5

@@ -536,12 +536,13 @@ def test_gemm_4bit_few_tokens_ragged_n(dev, nested, qt, bs, mnk):
 
 
 def test_gemm_4bit_library_knob_covers_few_tokens(dev, monkeypatch):
-    """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 forces the dequantise + GEMM pair for few tokens too (the few-token branch is not
-    taken): since round 4 the pair's GEMM is k_hgemm, so the result equals the forced "hgemm" route bit for bit and
+    """GEMM_4BIT_DEQUANT_MIN_ROWS = 1 and GEMM_4BIT_FEW_TOKENS = 0 force the dequantise + GEMM pair for few tokens too
+    (the few-token branch is not taken): since round 4 the pair's GEMM is k_hgemm, so the result equals the forced "hgemm" route bit for bit and
     dequantize_4bit + torch.matmul within the GEMM tolerance; the library GEMM stays reachable (_route="library")."""
     monkeypatch.setattr(_F(), "GEMM_4BIT_ROUTE_TUNING", False)
     F = _F()
     monkeypatch.setattr(F, "GEMM_4BIT_DEQUANT_MIN_ROWS", 1)
+    monkeypatch.setattr(F, "GEMM_4BIT_FEW_TOKENS", 0)
     M, N, K = 8, 2048, 1024
     torch.manual_seed(31)
     W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
