@@ -297,4 +297,16 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// roctx ranges around the C-ABI entry points (SURVEY §5's tracing plan: the only tracing hook a user of the drop-in
+// library gets).  Off unless BNB_ROCTX=1 is set when the library first checks: then libroctx64 is opened once
+// (dlopen, no link-time dependency) and every entry point pushes a range named after itself for the duration of the
+// call (host side: the launch, not the kernel; rocprofv3 --marker-trace records them).  Off, a range costs one load and
+// one branch.
+struct BnbRange {
+  bool on;
+  explicit BnbRange(const char* name);
+  ~BnbRange();
+};
+#define BNB_RANGE(name) ::bnb::BnbRange bnb_range_guard_(name)
+
 }  // namespace bnb

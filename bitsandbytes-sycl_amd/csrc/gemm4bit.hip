@@ -240,19 +240,23 @@ extern "C" {
 // Reference ABI slot (NF4 hard-coded, fp16), ref:sycl/pythonInterface.cpp:377-378.
 void cgemm_4bit_inference(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax, fp16_t* out, int lda,
                           int ldb, int ldc, int blocksize) {
+  BNB_RANGE("cgemm_4bit_inference");
   gemm_4bit<fp16_t>(m, n, k, A, B, absmax, nf4_table_device(), out, lda, ldb, ldc, blocksize);
 }
 // bf16 sibling and table-driven variants (any 16-entry code: NF4/FP4).
 void cgemm_4bit_inference_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, float* absmax, bf16_t* out, int lda,
                                int ldb, int ldc, int blocksize) {
+  BNB_RANGE("cgemm_4bit_inference_bf16");
   gemm_4bit<bf16_t>(m, n, k, A, B, absmax, nf4_table_device(), out, lda, ldb, ldc, blocksize);
 }
 void cgemm_4bit_inference_code_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax, float* datatype,
                                     fp16_t* out, int lda, int ldb, int ldc, int blocksize) {
+  BNB_RANGE("cgemm_4bit_inference_code_fp16");
   gemm_4bit<fp16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
 }
 void cgemm_4bit_inference_code_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, float* absmax, float* datatype,
                                     bf16_t* out, int lda, int ldb, int ldc, int blocksize) {
+  BNB_RANGE("cgemm_4bit_inference_code_bf16");
   gemm_4bit<bf16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
 }
 // [additive] the same with a caller-owned fp32 workspace that enables split-K for small tile grids
@@ -260,11 +264,13 @@ void cgemm_4bit_inference_code_bf16(int m, int n, int k, bf16_t* A, unsigned cha
 void cgemm_4bit_inference_code_ws_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax,
                                        float* datatype, fp16_t* out, int lda, int ldb, int ldc, int blocksize,
                                        float* workspace, long long workspace_bytes) {
+  BNB_RANGE("cgemm_4bit_inference_code_ws_fp16");
   gemm_4bit<fp16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, workspace, workspace_bytes);
 }
 void cgemm_4bit_inference_code_ws_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, float* absmax,
                                        float* datatype, bf16_t* out, int lda, int ldb, int ldc, int blocksize,
                                        float* workspace, long long workspace_bytes) {
+  BNB_RANGE("cgemm_4bit_inference_code_ws_bf16");
   gemm_4bit<bf16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize, workspace, workspace_bytes);
 }
 long long cgemm_4bit_workspace_bytes(int m, int n, int k) { return gemm_4bit_workspace_bytes(m, n, k); }

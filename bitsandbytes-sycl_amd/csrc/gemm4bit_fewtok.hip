@@ -558,6 +558,7 @@ template bool launch_gemm_4bit_fewtok<fp16_t>(int, int, int, const fp16_t*, int,
 extern "C" {
 // [lab, not in the header] timeline buffer of the ABL-128 variants (mode 16 + 128): 8 stamps per wave
 int cgemm_4bit_fewtok_timeline(unsigned long long* buf) {
+  BNB_RANGE("cgemm_4bit_fewtok_timeline");
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_ft_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
 // [additive, testing] whole-K few-token kernel: 0 = auto, 1 = off, 2 = wherever it fits
@@ -568,6 +569,7 @@ void cgemm_4bit_set_fewtok_mode(int mode) { bnb::g_fewtok_mode = mode; }
 // (the launch's own conditions: a lab mode (>= 16), an older few-token kernel (g_fewtoken_kernel) or a forced split-K
 // geometry (g_skinny_cfg) each keep the launch off this kernel, so the answer is 0 for them too)
 int cgemm_4bit_fewtok_takes(int m, int n, int k, int blocksize) {
+  BNB_RANGE("cgemm_4bit_set_fewtok_mode");
   if (bnb::g_fewtok_mode == 1 || bnb::g_fewtok_mode >= 16 || bnb::g_fewtoken_kernel != 0 || bnb::skinny_cfg_knob() >= 0 ||
       n < 1 || n > 32 || k < 64 || k % 64 || blocksize < 64 || (blocksize & (blocksize - 1)))
     return 0;

@@ -399,6 +399,7 @@ int cgemm_4bit_inference_nested_ws_bf16(int m, int n, int k, bf16_t* A, unsigned
                                         float* code2, float* absmax2, float* offset, float* datatype, bf16_t* out,
                                         int lda, int ldb, int ldc, int blocksize, int blocksize2, float* workspace,
                                         long long workspace_bytes) {
+  BNB_RANGE("cgemm_4bit_inference_nested_ws_bf16");
   SkStats st{nullptr, absmax_q, code2, absmax2, offset, 0, 0};
   if (m <= 0 || n <= 0) return 0;
   if (!launch_gemm_4bit_skinny<bf16_t>(m, n, k, A, lda, B, ldb, st, blocksize, blocksize2, datatype, out, ldc,
@@ -411,6 +412,7 @@ int cgemm_4bit_inference_nested_ws_fp16(int m, int n, int k, fp16_t* A, unsigned
                                         float* code2, float* absmax2, float* offset, float* datatype, fp16_t* out,
                                         int lda, int ldb, int ldc, int blocksize, int blocksize2, float* workspace,
                                         long long workspace_bytes) {
+  BNB_RANGE("cgemm_4bit_inference_nested_ws_fp16");
   SkStats st{nullptr, absmax_q, code2, absmax2, offset, 0, 0};
   if (m <= 0 || n <= 0) return 0;
   if (!launch_gemm_4bit_skinny<fp16_t>(m, n, k, A, lda, B, ldb, st, blocksize, blocksize2, datatype, out, ldc,

@@ -174,14 +174,17 @@ extern "C" {
 // the large-prefill 4-bit path (after cdequantize_blockwise_* / cdequantize_blockwise_nested_* into W), with the
 // per-shape solution search above.  Returns 0 on success, 1 on error (cget_last_error*).
 int cgemm_tn_bf16(int m, int n, int k, const bf16_t* A, int lda, const bf16_t* W, int ldw, bf16_t* C, int ldc) {
+  BNB_RANGE("cgemm_tn_bf16");
   return bnb::gemm_tn<rocblas_datatype_bf16_r>(m, n, k, A, lda, W, ldw, C, ldc);
 }
 int cgemm_tn_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* W, int ldw, fp16_t* C, int ldc) {
+  BNB_RANGE("cgemm_tn_fp16");
   return bnb::gemm_tn<rocblas_datatype_f16_r>(m, n, k, A, lda, W, ldw, C, ldc);
 }
 // [additive] solution search: on = 0 -> the standard algorithm only; budget_ms > 0 sets the per-shape search time;
 // clear != 0 forgets every cached plan.  Returns the number of cached plans.
 int cgemm_tn_set_search(int on, double budget_ms, int clear) {
+  BNB_RANGE("cgemm_tn_set_search");
   std::lock_guard<std::mutex> lock(bnb::g_mu);
   bnb::g_search = on;
   if (budget_ms > 0.0) bnb::g_budget_ms = budget_ms;
@@ -191,6 +194,7 @@ int cgemm_tn_set_search(int on, double budget_ms, int clear) {
 // [additive] the cached plan for (m, n, k, dtype 0 = bf16 / 1 = fp16, lda, ldw, ldc) on the current device: 1 = a
 // searched rocBLAS solution, 0 = the standard algorithm, -1 = not searched yet
 int cgemm_tn_plan(int m, int n, int k, int dtype, int lda, int ldw, int ldc) {
+  BNB_RANGE("cgemm_tn_plan");
   int dev = 0;
   hipGetDevice(&dev);
   std::lock_guard<std::mutex> lock(bnb::g_mu);

@@ -762,14 +762,17 @@ void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size
 
 void cgemm_4bit_inference_naive_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax, float* datatype,
                                      fp16_t* out, int lda, int ldb, int ldc, int blocksize) {
+  BNB_RANGE("cgemv_4bit_set_kernel");
   gemv_4bit<fp16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
 }
 void cgemm_4bit_inference_naive_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, float* absmax, float* datatype,
                                      bf16_t* out, int lda, int ldb, int ldc, int blocksize) {
+  BNB_RANGE("cgemm_4bit_inference_naive_bf16");
   gemv_4bit<bf16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
 }
 void cgemm_4bit_inference_naive_fp32(int m, int n, int k, float* A, unsigned char* B, float* absmax, float* datatype,
                                      float* out, int lda, int ldb, int ldc, int blocksize) {
+  BNB_RANGE("cgemm_4bit_inference_naive_fp32");
   gemv_4bit<float>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
 }
 
@@ -779,6 +782,7 @@ void cgemm_4bit_inference_naive_fp32(int m, int n, int k, float* A, unsigned cha
 int cgemm_4bit_inference_naive_nested_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, unsigned char* absmax_q,
                                            float* code2, float* absmax2, float* offset, float* datatype, fp16_t* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2) {
+  BNB_RANGE("cgemm_4bit_inference_naive_nested_fp16");
   (void)n; (void)lda; (void)ldc;
   GemvStats st{nullptr, absmax_q, code2, absmax2, offset, 0, 0};
   if (m <= 0) return 0;
@@ -790,6 +794,7 @@ int cgemm_4bit_inference_naive_nested_fp16(int m, int n, int k, fp16_t* A, unsig
 int cgemm_4bit_inference_naive_nested_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, unsigned char* absmax_q,
                                            float* code2, float* absmax2, float* offset, float* datatype, bf16_t* out,
                                            int lda, int ldb, int ldc, int blocksize, int blocksize2) {
+  BNB_RANGE("cgemm_4bit_inference_naive_nested_bf16");
   (void)n; (void)lda; (void)ldc;
   GemvStats st{nullptr, absmax_q, code2, absmax2, offset, 0, 0};
   if (m <= 0) return 0;

@@ -253,12 +253,14 @@ extern "C" {
 int cgemm_4bit_inference_tokens_bf16(int m, int ntok, int k, bf16_t* A, int lda, unsigned char* B, int ldb, float* absmax,
                                      unsigned char* absmax_q, float* code2, float* absmax2, float* offset,
                                      float* datatype, bf16_t* out, int ldc, int blocksize, int blocksize2) {
+  BNB_RANGE("cgemm_4bit_inference_tokens_bf16");
   return gemv_tokens<bf16_t>(m, ntok, k, A, lda, B, ldb, absmax, absmax_q, code2, absmax2, offset, datatype, out, ldc,
                              blocksize, blocksize2);
 }
 int cgemm_4bit_inference_tokens_fp16(int m, int ntok, int k, fp16_t* A, int lda, unsigned char* B, int ldb, float* absmax,
                                      unsigned char* absmax_q, float* code2, float* absmax2, float* offset,
                                      float* datatype, fp16_t* out, int ldc, int blocksize, int blocksize2) {
+  BNB_RANGE("cgemm_4bit_inference_tokens_fp16");
   return gemv_tokens<fp16_t>(m, ntok, k, A, lda, B, ldb, absmax, absmax_q, code2, absmax2, offset, datatype, out, ldc,
                              blocksize, blocksize2);
 }

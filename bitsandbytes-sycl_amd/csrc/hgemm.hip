@@ -797,9 +797,11 @@ extern "C" {
 // ref:python_src_quants/autograd/_functions.py:507).  Returns 0 = launched, 1 = shape / alignment not supported
 // (k % 64, 16-B aligned rows; nothing launched), 2 = launch error (cget_last_error*).
 int chgemm_tn_bf16(int m, int n, int k, const bf16_t* A, int lda, const bf16_t* W, int ldw, bf16_t* C, int ldc) {
+  BNB_RANGE("chgemm_tn_bf16");
   return bnb::hgemm_launch<bnb::HG_BF16>(m, n, k, A, lda, W, ldw, C, ldc);
 }
 int chgemm_tn_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* W, int ldw, fp16_t* C, int ldc) {
+  BNB_RANGE("chgemm_tn_fp16");
   return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc);
 }
 // [additive] the same with a caller workspace for split-K on small tile grids (< 192 tiles of 256 x 256: fp32
@@ -807,16 +809,19 @@ int chgemm_tn_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* 
 // bytes the shape needs (0: no split); a smaller workspace runs the unsplit kernel.
 int chgemm_tn_ws_bf16(int m, int n, int k, const bf16_t* A, int lda, const bf16_t* W, int ldw, bf16_t* C, int ldc,
                       float* ws, long long ws_bytes) {
+  BNB_RANGE("chgemm_tn_ws_bf16");
   return bnb::hgemm_launch<bnb::HG_BF16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
 }
 int chgemm_tn_ws_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* W, int ldw, fp16_t* C, int ldc,
                       float* ws, long long ws_bytes) {
+  BNB_RANGE("chgemm_tn_ws_fp16");
   return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
 }
 long long chgemm_tn_workspace_bytes(int m, int n, int k) { return bnb::hgemm_workspace_bytes(m, n, k, 2); }
 // [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k) with enough workspace: out = {WI, WJ, splits,
 // k-tiles per split}; the output tile is 32 WI x 32 WJ (256 x 256, 256 x 128 or 128 x 256)
 void chgemm_tn_plan(int m, int n, int k, int* out) {
+  BNB_RANGE("chgemm_tn_workspace_bytes");
   const bnb::HgPlan pl = bnb::hgemm_plan(m, n, k, 2, true, bnb::g_hgemm_variant == 1);
   out[0] = pl.wi;
   out[1] = pl.wj;
@@ -825,6 +830,7 @@ void chgemm_tn_plan(int m, int n, int k, int* out) {
 }
 // [additive, testing] k_hgemm schedule: 0 = the default, 1 = the A/B arm (HG_V_ALT); returns the previous setting
 int chgemm_set_variant(int v) {
+  BNB_RANGE("chgemm_set_variant");
   const int prev = bnb::g_hgemm_variant;
   bnb::g_hgemm_variant = v;
   return prev;

@@ -687,6 +687,7 @@ void cget_col_row_stats(fp16_t* A, float* rowStats, float* colStats, int* nnz_co
 // [additive] CA and row statistics in one pass (the row halves of cget_col_row_stats + cdouble_rowcol_quant,
 // threshold 0).  Returns 0 when launched, 1 when the shape needs the two-kernel path.
 int cint8_row_quant_fp16(fp16_t* A, float* rowStats, char* out_row, int rows, int cols) {
+  BNB_RANGE("cint8_row_quant_fp16");
   if (rows <= 0 || cols <= 0) return 0;
   if (cols % 8 || cols > 64 * 8 * RQ_MAX_VEC || ((uintptr_t)A & 15) || ((uintptr_t)out_row & 7)) return 1;
   const int per_lane = (cols / 8 + 63) / 64;
@@ -707,6 +708,7 @@ int cint8_row_quant_fp16(fp16_t* A, float* rowStats, char* out_row, int rows, in
 
 void cdouble_rowcol_quant(fp16_t* A, float* rowStats, float* colStats, char* out_col_normed, char* out_row_normed,
                           int* rowidx, int* colidx, fp16_t* val, int* nnz_row_ptr, float threshold, int rows, int cols) {
+  BNB_RANGE("cdouble_rowcol_quant");
   if (rows <= 0 || cols <= 0) return;
   const int col_tiles = (cols + 255) / 256, row_tiles = (rows + 15) / 16;
   const bool vec = (((uintptr_t)A & 15) == 0) && (cols % 8 == 0) && (((uintptr_t)out_col_normed & 7) == 0) &&
@@ -738,21 +740,27 @@ void ctransform_turing2row(char* A, char* out, int rows, int cols) { launch_tran
 void ctransform_ampere2row(char* A, char* out, int rows, int cols) { launch_transform<AMPERE, false, true>((int8_t*)A, (int8_t*)out, rows, cols); }
 
 int cigemmlt_turing_32(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemmlt_turing_32");
   return launch_igemm<COL32, TURING, EPI_I32_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
 }
 int cigemmlt_turing_8(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemmlt_turing_8");
   return launch_igemm<COL32, TURING, EPI_I8_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
 }
 int cigemmlt_turing_8_rowscale(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemmlt_turing_8_rowscale");
   return launch_igemm<COL32, TURING, EPI_I8_COL32_ROWSCALE>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
 }
 int cigemmlt_ampere_32(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemmlt_ampere_32");
   return launch_igemm<COL32, AMPERE, EPI_I32_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
 }
 int cigemmlt_ampere_8(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemmlt_ampere_8");
   return launch_igemm<COL32, AMPERE, EPI_I8_COL32>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
 }
 int cigemmlt_ampere_8_rowscale(int m, int n, int k, const int8_t* A, const int8_t* B, void* C, float* row_scale, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemmlt_ampere_8_rowscale");
   return launch_igemm<COL32, AMPERE, EPI_I8_COL32_ROWSCALE>(m, n, k, A, B, C, row_scale, lda, ldb, ldc);
 }
 
@@ -760,10 +768,12 @@ int cigemmlt_ampere_8_rowscale(int m, int n, int k, const int8_t* A, const int8_
 // row-major out [m, n] (ldc), i.e. igemmlt + cdequant_mm_int32_fp16 fused into one launch.
 int cigemmlt_row_dequant_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, fp16_t* out, const float* rowStats,
                               const float* colStats, const fp16_t* bias, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemmlt_row_dequant_fp16");
   return launch_igemm<ROW, ROW, EPI_F16_ROW_DEQUANT>(m, n, k, A, B, out, nullptr, lda, ldb, ldc, rowStats, colStats, bias);
 }
 // Additive: row-major int8 GEMM with int32 row-major output (exact igemm, test_matmulqlt.py:194-204).
 int cigemm_row_i32(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc) {
+  BNB_RANGE("cigemm_row_i32");
   return launch_igemm<ROW, ROW, EPI_I32_ROW>(m, n, k, A, B, out, nullptr, lda, ldb, ldc);
 }
 // Additive: the two row-major entry points with a caller workspace (size: cigemmlt_workspace_bytes) that lets
@@ -771,11 +781,13 @@ int cigemm_row_i32(int m, int n, int k, const int8_t* A, const int8_t* B, int32_
 int cigemmlt_row_dequant_ws_fp16(int m, int n, int k, const int8_t* A, const int8_t* B, fp16_t* out,
                                  const float* rowStats, const float* colStats, const fp16_t* bias, int lda, int ldb,
                                  int ldc, int32_t* workspace, long long workspace_bytes) {
+  BNB_RANGE("cigemmlt_row_dequant_ws_fp16");
   return launch_igemm<ROW, ROW, EPI_F16_ROW_DEQUANT>(m, n, k, A, B, out, nullptr, lda, ldb, ldc, rowStats, colStats,
                                                      bias, workspace, workspace_bytes);
 }
 int cigemm_row_i32_ws(int m, int n, int k, const int8_t* A, const int8_t* B, int32_t* out, int lda, int ldb, int ldc,
                       int32_t* workspace, long long workspace_bytes) {
+  BNB_RANGE("cigemm_row_i32_ws");
   return launch_igemm<ROW, ROW, EPI_I32_ROW>(m, n, k, A, B, out, nullptr, lda, ldb, ldc, nullptr, nullptr, nullptr,
                                              workspace, workspace_bytes);
 }
@@ -783,6 +795,7 @@ long long cigemmlt_workspace_bytes(int m, int n, int k) { return igemm_workspace
 
 void cdequant_mm_int32_fp16(int* A, float* rowStats, float* colStats, fp16_t* out, float* newRowStats,
                             float* newcolStats, fp16_t* bias, int numRows, int numCols) {
+  BNB_RANGE("cdequant_mm_int32_fp16");
   (void)newRowStats; (void)newcolStats;   // unused by the reference kernel as well
   if (numRows <= 0 || numCols <= 0) return;
   if (numCols % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)colStats & 15) == 0 &&

@@ -92,12 +92,14 @@ extern "C" {
 
 // [additive] bytes of one rank's exchange buffer for `world` ranks and n elements of `elem` bytes per shard
 long long cipc_allgather_buffer_bytes(int world, int n, int elem) {
+  BNB_RANGE("cipc_allgather_buffer_bytes");
   return bnb::IPC_FLAG_BYTES + 2LL * world * bnb::ipc_slot_bytes(n, elem);
 }
 
 // [additive] allocate a zeroed exchange buffer (uncached device memory; fine-grained, then plain hipMalloc as
 // fallbacks); *kind = 2 uncached, 1 fine-grained, 0 plain.  Returns the device pointer or NULL (cget_last_error*).
 void* cipc_alloc(long long bytes, int* kind) {
+  BNB_RANGE("cipc_alloc");
   void* p = nullptr;
   int k = 2;
   if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess) {
@@ -122,6 +124,7 @@ void* cipc_alloc(long long bytes, int* kind) {
 }
 
 void cipc_free(void* p) {
+  BNB_RANGE("cipc_free");
   if (p) (void)hipFree(p);
 }
 
@@ -129,6 +132,7 @@ int cipc_handle_size() { return HIP_IPC_HANDLE_SIZE; }
 
 // [additive] the IPC handle of a cipc_alloc buffer into `handle` (cipc_handle_size() bytes); 0 = ok
 int cipc_get_handle(void* p, void* handle) {
+  BNB_RANGE("cipc_get_handle");
   hipIpcMemHandle_t h;
   const hipError_t e = hipIpcGetMemHandle(&h, p);
   if (e != hipSuccess) {
@@ -141,6 +145,7 @@ int cipc_get_handle(void* p, void* handle) {
 
 // [additive] open a peer's handle; the mapped device pointer goes to *out; 0 = ok
 int cipc_open_handle(const void* handle, void** out) {
+  BNB_RANGE("cipc_open_handle");
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle, sizeof(h));
   const hipError_t e = hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
@@ -160,6 +165,7 @@ int cipc_close_handle(void* p) { return hipIpcCloseMemHandle(p) == hipSuccess ? 
 // 16 (whole 16-B pieces; n % 8 == 0).
 int callgather_ipc_16(const unsigned long long* bufs, int rank, int world, int n, const void* y, void* rows,
                       unsigned* state) {
+  BNB_RANGE("callgather_ipc_16");
   if (world < 1 || world > bnb::IPC_MAX_RANKS || rank < 0 || rank >= world || n <= 0 || n % 8 ||
       ((uintptr_t)y & 15) || ((uintptr_t)rows & 15))
     return 1;

@@ -473,6 +473,7 @@ extern "C" {
                                               float beta1, float beta2, float eps, int step, float lr,             \
                                               float* quantiles1, float* quantiles2, float* absmax1, float* absmax2, \
                                               float weight_decay, const float gnorm_scale, bool skip_zeros, int n) { \
+    BNB_RANGE("c" #fname "_8bit_blockwise_grad_" #gbits);                                                         \
     optimizer_8bit_blockwise<gtype, OPT>(p, g, state1, state2, beta1, beta2, eps, step, lr, quantiles1, quantiles2, \
                                          absmax1, absmax2, weight_decay, gnorm_scale, skip_zeros, n);              \
   }
@@ -498,6 +499,7 @@ BNB_BLOCKWISE8(lion, LION, bf16_t, bf16)
                                     float max_unorm, float param_norm, const float beta1, const float beta2,    \
                                     const float eps, const float weight_decay, const int step, const float lr,  \
                                     const float gnorm_scale, bool skip_zeros, const int n) {                    \
+    BNB_RANGE("c" #fname "32bit_grad_" #gbits);                                                              \
     optimizer_32bit<gtype, OPT>(g, p, state1, state2, unorm, max_unorm, param_norm, beta1, beta2, eps,          \
                                 weight_decay, step, lr, gnorm_scale, skip_zeros, n);                            \
   }

@@ -106,6 +106,7 @@ extern "C" {
 // 8-wave workgroups (two waves per SIMD) instead of 4: `blocks` workgroups, every wave issues 8 x iters MFMAs;
 // sink >= blocks * 512 floats.  Returns 0 / 1 (bad kind) / 2 (launch).
 int cprobe_mfma(int kind, int blocks, int iters, unsigned seed, float* sink) {
+  BNB_RANGE("cprobe_mfma");
   const int threads = (kind & 2) ? 512 : 256;
   if ((kind & 1) == 0)
     hipLaunchKernelGGL((bnb::k_probe_mfma<0>), dim3(blocks), dim3(threads), 0, bnb::current_stream(), iters, seed, sink);
@@ -118,6 +119,7 @@ int cprobe_mfma(int kind, int blocks, int iters, unsigned seed, float* sink) {
 // [additive, measurement] streaming read of `bytes` (multiple of 16) at p by `blocks` workgroups of 256 threads;
 // sink >= blocks dwords.
 int cprobe_hbm_read(const void* p, long long bytes, int blocks, unsigned* sink) {
+  BNB_RANGE("cprobe_hbm_read");
   hipLaunchKernelGGL(bnb::k_probe_hbm_read, dim3(blocks), dim3(256), 0, bnb::current_stream(),
                      reinterpret_cast<const bnb::pb_u32x4_t*>(p), bytes / 16, sink);
   return hipGetLastError() == hipSuccess ? 0 : 2;
@@ -125,11 +127,13 @@ int cprobe_hbm_read(const void* p, long long bytes, int blocks, unsigned* sink) 
 
 // [additive, testing] fill the LDS of every CU with `pattern` (blocks: >= the CU count; one launch on the current stream)
 int cprobe_lds_poison(unsigned pattern, int blocks) {
+  BNB_RANGE("cprobe_lds_poison");
   hipLaunchKernelGGL(k_probe_lds_poison, dim3(blocks), dim3(256), 0, bnb::current_stream(), pattern);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 // [additive, testing] positive control of the poisoning: out[b * 256 + t] = an LDS word the kernel never wrote
 int cprobe_lds_peek(unsigned* out, int blocks) {
+  BNB_RANGE("cprobe_lds_peek");
   hipLaunchKernelGGL(k_probe_lds_peek, dim3(blocks), dim3(256), 0, bnb::current_stream(), out);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

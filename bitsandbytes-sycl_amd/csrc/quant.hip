@@ -480,10 +480,12 @@ extern "C" {
 
 #define BNB_QUANT_ABI(fname, T, DT)                                                                   \
   void fname(float* code, T* A, float* absmax, unsigned char* out, int blocksize, const int n) {     \
+    BNB_RANGE(#fname);                                                                                \
     quantize_blockwise<T, DT>(code, A, absmax, out, blocksize, n);                                    \
   }
 #define BNB_DEQUANT_ABI(fname, T, DT)                                                                 \
   void fname(float* code, unsigned char* A, float* absmax, T* out, int blocksize, const int n) {     \
+    BNB_RANGE(#fname);                                                                                \
     dequantize_blockwise<T, DT>(code, A, absmax, out, blocksize, n);                                  \
   }
 
@@ -513,6 +515,7 @@ BNB_DEQUANT_ABI(cdequantize_blockwise_fp32_nf4, float, NF4)
 #define BNB_DEQUANT_NESTED_ABI(fname, T, DT)                                                                    \
   int fname(unsigned char* A, unsigned char* absmax_q, float* code2, float* absmax2, float* offset, T* out,      \
             int blocksize, int blocksize2, long long n) {                                                        \
+    BNB_RANGE(#fname);                                                                                            \
     return dequantize_4bit_nested<T, DT>(A, absmax_q, code2, absmax2, offset, out, blocksize, blocksize2, n) ? 0  \
                                                                                                              : 1; \
   }
@@ -529,6 +532,7 @@ BNB_DEQUANT_NESTED_ABI(cdequantize_blockwise_nested_bf16_nf4, bf16_t, NF4)
 // rewritten (the kernel uses code[0] = -1 internally).
 void cquantize_blockwise_bytes_fp32(float* code, float* A, float* absmax, unsigned char* out, long long blocksize,
                                     long long n) {
+  BNB_RANGE("cquantize_blockwise_bytes_fp32");
   if (n <= 0 || blocksize <= 0) return;
   const long long nb = (n + blocksize - 1) / blocksize;
   if (nb > 0x7fffffffLL) { set_error(1, "quantize_bytes: too many blocks"); return; }
@@ -541,6 +545,7 @@ void cquantize_blockwise_bytes_fp32(float* code, float* A, float* absmax, unsign
 // offset add of functional.py:1346-1350); blocksize2 must be a power of two.
 void cdequantize_nested_absmax_fp32(float* code2, unsigned char* q, float* absmax2, float* offset, float* out,
                                     int blocksize2, long long n) {
+  BNB_RANGE("cdequantize_nested_absmax_fp32");
   if (n <= 0) return;
   if (blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1))) {
     set_error(1, "dequantize_nested_absmax: blocksize2 must be a power of two");
@@ -556,6 +561,7 @@ void cdequantize_nested_absmax_fp32(float* code2, unsigned char* q, float* absma
 // used by the config-1 GPU measurement.  Not in the reference ABI.
 void cdequantize_blockwise_bytes_fp32(float* code, unsigned char* A, float* absmax, float* out, long long blocksize,
                                       long long n) {
+  BNB_RANGE("cdequantize_blockwise_bytes_fp32");
   if (n <= 0 || blocksize <= 0) return;
   hipLaunchKernelGGL(k_dequantize_cpu_semantics, dim3(stream_grid(n, 256)), dim3(256), 0, current_stream(), code, A,
                      absmax, out, blocksize, n);

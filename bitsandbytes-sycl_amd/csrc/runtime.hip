@@ -16,6 +16,8 @@
 #include <cstring>
 #include <mutex>
 
+#include <dlfcn.h>
+
 namespace bnb {
 
 static thread_local hipStream_t g_stream = nullptr;
@@ -30,6 +32,33 @@ void set_error(int code, const char* what) {
   std::lock_guard<std::mutex> lk(g_err_mu);
   std::snprintf(g_err_msg, sizeof(g_err_msg), "%s (code %d)", what, code);
   if (std::getenv("BNB_HIP_VERBOSE")) std::fprintf(stderr, "[bnb-hip] %s\n", g_err_msg);
+}
+
+typedef int (*roctx_push_fn)(const char*);
+typedef int (*roctx_pop_fn)();
+struct RoctxApi {
+  roctx_push_fn push = nullptr;
+  roctx_pop_fn pop = nullptr;
+  RoctxApi() {
+    const char* e = std::getenv("BNB_ROCTX");
+    if (!e || std::strcmp(e, "1") != 0) return;
+    void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    push = reinterpret_cast<roctx_push_fn>(dlsym(h, "roctxRangePushA"));
+    pop = reinterpret_cast<roctx_pop_fn>(dlsym(h, "roctxRangePop"));
+    if (!push || !pop) push = nullptr, pop = nullptr;
+  }
+};
+static const RoctxApi& roctx_api() {
+  static const RoctxApi api;   // thread-safe one-time init
+  return api;
+}
+BnbRange::BnbRange(const char* name) : on(roctx_api().push != nullptr) {
+  if (on) roctx_api().push(name);
+}
+BnbRange::~BnbRange() {
+  if (on) roctx_api().pop();
 }
 
 }  // namespace bnb
@@ -73,5 +102,8 @@ int cget_last_error() { return bnb::g_last_error.exchange(0); }
 const char* cget_last_error_message() { return bnb::g_err_msg; }
 
 int cget_abi_version() { return 1; }
+
+// [additive] 1 when roctx ranges are on (BNB_ROCTX=1 and libroctx64 found), else 0
+int croctx_enabled() { return bnb::roctx_api().push != nullptr ? 1 : 0; }
 
 }  // extern "C"

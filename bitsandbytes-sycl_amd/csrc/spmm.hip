@@ -112,6 +112,7 @@ extern "C" {
 void cspmm_coo_very_sparse_naive_fp16(int* max_count, int* max_idx, int* offset_rowidx, int* rowidx, int* colidx,
                                       fp16_t* values, fp16_t* B, fp16_t* out, float* dequant_stats, int nnz_rows,
                                       int nnz, int rowsA, int rowsB, int colsB) {
+  BNB_RANGE("cspmm_coo_very_sparse_naive_fp16");
   (void)nnz; (void)rowsA; (void)rowsB;
   spmm_coo_very_sparse<fp16_t>(max_count, max_idx, offset_rowidx, rowidx, colidx, values, B, out, dequant_stats,
                                nnz_rows, colsB);
@@ -119,6 +120,7 @@ void cspmm_coo_very_sparse_naive_fp16(int* max_count, int* max_idx, int* offset_
 void cspmm_coo_very_sparse_naive_int8(int* max_count, int* max_idx, int* offset_rowidx, int* rowidx, int* colidx,
                                       fp16_t* values, signed char* B, fp16_t* out, float* dequant_stats, int nnz_rows,
                                       int nnz, int rowsA, int rowsB, int colsB) {
+  BNB_RANGE("cspmm_coo_very_sparse_naive_int8");
   (void)nnz; (void)rowsA; (void)rowsB;
   spmm_coo_very_sparse<int8_t>(max_count, max_idx, offset_rowidx, rowidx, colidx, values, (int8_t*)B, out,
                                dequant_stats, nnz_rows, colsB);
@@ -129,6 +131,7 @@ void cspmm_coo_very_sparse_naive_int8(int* max_count, int* max_idx, int* offset_
 // (functional.py:2656-2701).  Every row of C is written (0 for empty rows).
 void cspmm_coo_rows(int* row_ptr, int* A_colidx, fp16_t* A_vals, int A_rows, int B_cols, int ldb, fp16_t* B, int ldc,
                     fp16_t* C, bool transposed_B) {
+  BNB_RANGE("cspmm_coo_rows");
   if (A_rows <= 0 || B_cols <= 0) return;
   hipLaunchKernelGGL(k_spmm_coo_rows, dim3(A_rows), dim3(SPMM_THREADS), 0, current_stream(), row_ptr, A_colidx, A_vals,
                      B, C, B_cols, ldb, ldc, transposed_B);

@@ -410,6 +410,7 @@ void* cget_stream(void);
 int cget_last_error(void);                 /* returns and clears the last error code (0 = none) */
 const char* cget_last_error_message(void);
 int cget_abi_version(void);
+int croctx_enabled(void);                  /* 1 when roctx ranges are on: BNB_ROCTX=1 at load and libroctx64 found */
 
 #ifdef __cplusplus
 }

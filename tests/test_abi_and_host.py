@@ -140,3 +140,19 @@ def test_route_rows_bucket():
     for r in range(1, 5000, 7):
         b = F._route_rows_bucket(r)
         assert b <= r and r - b < max(1, r // 4 + 1)
+
+
+def test_roctx_ranges_switch():
+    """roctx ranges around the C-ABI entry points (SURVEY §5 tracing plan) are off by default and on with
+    BNB_ROCTX=1 (libroctx64 opened at run time); checked in fresh processes, no GPU needed."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0] = [%r]; import python_src_quants.functional as F; "
+            "print(F.lib.croctx_enabled())" % os.path.join(ROOT, "bitsandbytes-sycl_amd"))
+    env = dict(os.environ)
+    env.pop("BNB_ROCTX", None)
+    off = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    env["BNB_ROCTX"] = "1"
+    on = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert off.stdout.strip().splitlines()[-1] == "0", off.stderr[-500:]
+    assert on.stdout.strip().splitlines()[-1] == "1", on.stderr[-500:]
