@@ -19,6 +19,9 @@ namespace bnb {
 hipStream_t current_stream() { return nullptr; }
 void set_error(int, const char* what) { printf("error: %s\n", what); }
 int g_tile_override = 0;
+BnbRange::BnbRange(const char*) : on(false) {}
+BnbRange::~BnbRange() {}
+int device_cu_count() { return 256; }
 template <typename T> void launch_splitk_rows_reduce(const float*, int, int, int, T*, int) {}   // split-K unused here
 template void launch_splitk_rows_reduce<bf16_t>(const float*, int, int, int, bf16_t*, int);
 template void launch_splitk_rows_reduce<fp16_t>(const float*, int, int, int, fp16_t*, int);
@@ -33,7 +36,7 @@ static float bf2f(uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(
 template <int... Vs> struct Variants {
   template <class F> static void each(F f) { (f(std::integral_constant<int, Vs>{}), ...); }
 };
-using LabV = Variants<8 + 16 + 4096, 16 + 8192>;
+using LabV = Variants<16 + 8192, 8 + 16 + 4096>;
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096, K = argc > 3 ? atoi(argv[3]) : 11008;
