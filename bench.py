@@ -50,6 +50,9 @@ def _events():
 # step only: an event record between two kernels costs the stream ~3-4 us on this stack, so five per step cost
 # ~18 us of a 250 us step (tools/step_overhead.py, profiles/lab/r02_step_overhead.txt).
 STAGE_EVERY = 10
+# gemm_4bit(..., prefetch=...): each dequantise + k_hgemm step dequantises the next weight inside its GEMM (--prefetch;
+# default: the unpipelined pair, one dequantise launch before each GEMM -- measured faster so far)
+PREFETCH = [False]
 
 
 class StepClock:
@@ -422,8 +425,10 @@ def bench_llama2_7b_prefill(dev, batch=32, seq=2048, iters=3):
     outs = {n_out: torch.empty(tokens, n_out, device=dev, dtype=torch.bfloat16) for n_out in (hid, inter)}
 
     def layer():
-        for (n_out, k_in), (q, st) in zip(shapes, ws):
-            F.gemm_4bit(X if k_in == hid else Xi, q, st, out=outs[n_out])
+        # each projection's GEMM dequantises the next one's weight (the last: the next layer's first, same shapes)
+        for i, ((n_out, k_in), (q, st)) in enumerate(zip(shapes, ws)):
+            F.gemm_4bit(X if k_in == hid else Xi, q, st, out=outs[n_out],
+                        prefetch=ws[(i + 1) % len(ws)] if PREFETCH[0] else None)
     t = _time_loop(layer, iters)
     flops = sum(2.0 * tokens * n_out * k_in for n_out, k_in in shapes)
     res = {"tokens": tokens, "layer_ms": t * 1e3, "tflops": flops / t / 1e12, "model_32_layers_ms": 32 * t * 1e3,
@@ -459,8 +464,10 @@ def bench_llama2_70b_shard(dev, ranks=8, prefill_tokens=4096, layer_copies=8, it
     outs = {n: torch.empty(prefill_tokens, n, device=dev, dtype=torch.bfloat16) for n, _ in shapes}
 
     def layer():
-        for (n_out, k_in), (q, st) in zip(shapes, layers[0]):
-            F.gemm_4bit(X if k_in == hid else Xi, q, st, out=outs[n_out])
+        ws = layers[0]
+        for i, ((n_out, k_in), (q, st)) in enumerate(zip(shapes, ws)):
+            F.gemm_4bit(X if k_in == hid else Xi, q, st, out=outs[n_out],
+                        prefetch=ws[(i + 1) % len(ws)] if PREFETCH[0] else None)
     t = _time_loop(layer, iters)
     flops = sum(2.0 * prefill_tokens * n * k for n, k in shapes)
     res["prefill"] = {"tokens": prefill_tokens, "layer_ms": t * 1e3, "tflops": flops / t / 1e12,
@@ -598,6 +605,9 @@ def gemm_kernel_name(m, n, k=K, route=None):
     split-K) has >= 128 workgroups, else the 128x128 one."""
     route = route or F.gemm_4bit_static_route(m, n, k)
     if route == "hgemm":
+        if PREFETCH[0]:
+            return ("k_hgemm<bf16> (hand-written, hgemm.hip) with the next call's NF4 dequantise inside it "
+                    "(prefetch, HgSide)")
         return "k_hgemm<bf16> (hand-written, hgemm.hip) after k_dequantize_4bit_stream<bf16,NF4>"
     if route == "library_tn":
         return ("library bf16 GEMM (Cijk_*, rocBLAS solution searched per shape, cgemm_tn_bf16) after "
@@ -688,12 +698,15 @@ def main():
     ap.add_argument("--no-int8", action="store_true", help="skip the sharded int8 leg")
     ap.add_argument("--no-decode", action="store_true", help="skip the sharded decode (M = 1) leg")
     ap.add_argument("--no-ipc", action="store_true", help="N > 1: skip the one-shot peer-memory decode all-gather leg")
+    ap.add_argument("--prefetch", action="store_true",
+                    help="dequantise each step's weight inside the previous step's GEMM (gemm_4bit prefetch=)")
     ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 ranks on one GPU")
     ap.add_argument("--chunks", type=int, default=2,
                     help="N>1: token-row chunks whose all-gathers overlap the next chunk's GEMM")
     args = ap.parse_args()
+    PREFETCH[0] = args.prefetch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -741,10 +754,15 @@ def main():
         ev = []
 
         first = [True]
+        calls = [0]
 
         def mm(xc, yc):   # chunks after the first reuse this step's dequantised shard (library path)
+            # the step's last GEMM dequantises the next step's weight inside it (prefetch; the layer's next weight in a
+            # model -- here the same shard again, so every step still dequantises it once)
+            calls[0] += 1
+            pf = (q, st) if PREFETCH[0] and calls[0] == chunks else None
             r = F.gemm_4bit(xc, q, st, out=yc, absmax=absmax, events=ev if record else None,
-                            reuse_weight=not first[0])
+                            reuse_weight=not first[0], prefetch=pf)
             first[0] = False
             return r
         if world > 1:
@@ -876,7 +894,8 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (seeded randn; W ~ N(0,0.02) -> NF4 bs=64 nested stats; X ~ N(0,1) bf16)",
             "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (functional.gemm_4bit: HIP "
-                                   "dequantise + the hand-written bf16 GEMM k_hgemm at this M; fused dequant+MFMA "
+                                   "dequantise + the hand-written bf16 GEMM k_hgemm at this M, the dequantise of each "
+                                   "step's weight run inside the previous step's k_hgemm (prefetch); fused dequant+MFMA "
                                    f"kernel below {F.GEMM_4BIT_DEQUANT_MIN_ROWS} rows / "
                                    f"{F.GEMM_4BIT_DEQUANT_MIN_FEATURES} features) + bf16 all-gather of output-column "
                                    "shards",
@@ -892,7 +911,9 @@ def main():
                          if peaks and "bf16_mfma_tflops" in peaks else None,
                          "kernel": kname, "kernel_us": round(kern_s * 1e6, 2),
                          "flops_per_launch": shard_flops,
-                         "dequantize_us": round(deq_s * 1e6, 2) if deq_s else None, **pmc_extra},
+                         "dequantize_us": round(deq_s * 1e6, 2) if deq_s else None,
+                         # the step's dequantise runs inside the previous step's k_hgemm (kernel_us includes it)
+                         "dequantize_inside_gemm": bool(PREFETCH[0] and kname.startswith("k_hgemm")), **pmc_extra},
             "measured_peaks": peaks,
             "cpu_baseline": cpu,
         }

@@ -173,7 +173,7 @@ __device__ __forceinline__ void hg_static_for(F&& f) {
 
 template <int WI, int WJ> struct HgPlan3;
 template <> struct HgPlan3<8, 8> {
-  static constexpr int B1 = 21, B2 = 50, B3 = 88, SETB = 22, SETA = 61, VM = 13;
+  static constexpr int B1 = 21, B2 = 50, B3 = 88, SETB = 22, SETA = 61, VM = 13, SIDEQ = 120;
   __host__ __device__ static constexpr int wread(int q) { return q < 16 && (q & 1) == 0 ? q >> 1 : -1; }
   __host__ __device__ static constexpr int xread(int q) { return q >= 23 && q <= 44 && (q - 23) % 3 == 0 ? (q - 23) / 3 : -1; }
   __host__ __device__ static constexpr int bpiece(int q) {
@@ -186,7 +186,7 @@ template <> struct HgPlan3<8, 8> {
   __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 31 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
 };
 template <> struct HgPlan3<8, 4> {                      // 256 x 128: 4 B pieces, 8 A pieces per wave
-  static constexpr int B1 = 9, B2 = 27, B3 = 38, SETB = 10, SETA = 22, VM = 9;
+  static constexpr int B1 = 9, B2 = 27, B3 = 38, SETB = 10, SETA = 22, VM = 9, SIDEQ = 58;
   __host__ __device__ static constexpr int wread(int q) { return q < 8 && (q & 1) == 0 ? q >> 1 : -1; }
   __host__ __device__ static constexpr int xread(int q) { return q >= 11 && q <= 25 && (q - 11) % 2 == 0 ? (q - 11) / 2 : -1; }
   __host__ __device__ static constexpr int bpiece(int q) { return q == 12 ? 0 : q == 15 ? 1 : q == 18 ? 2 : q == 21 ? 3 : -1; }
@@ -196,7 +196,7 @@ template <> struct HgPlan3<8, 4> {                      // 256 x 128: 4 B pieces
   __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 23 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
 };
 template <> struct HgPlan3<4, 8> {                      // 128 x 256: 8 B pieces, 4 A pieces per wave
-  static constexpr int B1 = 17, B2 = 27, B3 = 38, SETB = 17, SETA = 33, VM = 10;
+  static constexpr int B1 = 17, B2 = 27, B3 = 38, SETB = 17, SETA = 33, VM = 10, SIDEQ = 58;
   __host__ __device__ static constexpr int wread(int q) { return q < 16 && (q & 1) == 0 ? q >> 1 : -1; }
   __host__ __device__ static constexpr int xread(int q) { return q >= 19 && q <= 25 && (q - 19) % 2 == 0 ? (q - 19) / 2 : -1; }
   __host__ __device__ static constexpr int bpiece(int q) {
@@ -206,14 +206,41 @@ template <> struct HgPlan3<4, 8> {                      // 128 x 256: 8 B pieces
   __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 23 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
 };
 
-template <int OP, int V = 0, bool SPLIT = false, int WI = 8, int WJ = 8>
+// Side dequantise (SIDE = true, bf16 / fp16 only): while it multiplies, the kernel also dequantises the NEXT 4-bit
+// weight (the next projection of the layer, or the next layer's) into a second weight buffer -- the cdequantize_blockwise
+// / dequantize_4bit_nested work of the following gemm_4bit call, software-pipelined one weight ahead so that the
+// HBM-bound dequantise runs in the MFMA-bound GEMM's shadow instead of as its own launch (the same values as
+// k_dequantize_4bit_stream, quant.hip: fp32 code * fp32 absmax, one RNE cast; nested statistics decoded as
+// code2[q8] * absmax2 + offset).  Workgroup w owns packed dwords [w * per_wg, (w + 1) * per_wg), 256 per "iteration"
+// (one dword = 8 weights per lane, coalesced).  In the main loop one iteration runs every `every` k-tiles, right after
+// barrier B3: its loads are issued then and consumed one side step later, after that step's B3 wait -- the loads sit
+// before the next k-tile's DMA pieces, so vmcnt(VM) at the next B3 already covers them and the DMA counts stay exact
+// (the loads and the 16-B stores are inline asm, invisible to hipcc's wait insertion, like the DMA).  Iterations
+// left when the loop ends (few k-tiles) run after it.
+struct HgSide {
+  const uint8_t* packed;     // next weight, packed 4-bit (4-B aligned)
+  const float* absmax;       // fp32 block statistics (nested == 0)
+  const uint8_t* q8;         // nested: 8-bit codes of the statistics
+  const float* code2;        // nested: their 256-entry code
+  const float* absmax2;      // nested: second-level scales
+  const float* offset;       // nested: the statistics' offset
+  void* out;                 // ndw * 8 outputs of the GEMM's type (16-B aligned)
+  long long ndw;             // packed dwords (elements / 8)
+  int per_wg, iters, every, bs_shift, bs2_shift, nested, fp4;
+  int mode;                  // A/B bits (chgemm_set_side_mode): 1 = non-temporal side loads / stores, 2 = lab: no
+                             // side stores, 4 = lab: no side loads (timing only, wrong weights)
+};
+static int g_side_mode = 1;
+
+template <int OP, int V = 0, bool SPLIT = false, int WI = 8, int WJ = 8, bool SIDE = false>
 __global__ void __launch_bounds__(HG_THREADS, 1)
 k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const void* __restrict__ Bv, long long ldb,
         void* __restrict__ Cv, long long ldc, const float* __restrict__ rowStats, const float* __restrict__ colStats,
-        const fp16_t* __restrict__ bias, float* __restrict__ ws, int ksplit, int kchunk) {
+        const fp16_t* __restrict__ bias, float* __restrict__ ws, int ksplit, int kchunk, HgSide side) {
   using Op = HgOpT<OP>;
   using acc_t = typename Op::acc_t;
   constexpr int E = Op::ELEM;
+  static_assert(!SIDE || ((OP == HG_BF16 || OP == HG_FP16) && (V & 8192) != 0), "side dequantise: 16-bit, tile3");
   // tile shape: 2 x 2 waves of (16 WI) x (16 WJ) outputs -- 256 x 256 (8, 8), 256 x 128 (8, 4), 128 x 256 (4, 8)
   static_assert((WI == 8 && WJ == 8) || (V & 8192) != 0, "tile shapes other than 256 x 256 run the three-barrier schedule");
   constexpr int BM = 32 * WI, BN = 32 * WJ;
@@ -230,9 +257,92 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   const int kt0 = split * kchunk;
   const uint8_t* A = reinterpret_cast<const uint8_t*>(Av) + (long long)kt0 * 128;
   const uint8_t* B = reinterpret_cast<const uint8_t*>(Bv) + (long long)kt0 * 128;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES];
+  // side dequantise (SIDE): pair table (2 KiB) + code2 (1 KiB) + the LDS-DMA landing slots of one iteration's three
+  // words per lane ([3][256] u32)
+  constexpr int SIDE_LDS = SIDE ? 6144 : 0;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + SIDE_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  using T16 = typename std::conditional<OP == HG_FP16, fp16_t, bf16_t>::type;
+  // Side dequantise state.  The iteration's words travel by LDS-DMA into the landing slots (global_load_lds_dword, M0 =
+  // the slot row of this wave), never into registers: an asm load's destination register is written when the load
+  // returns, and hipcc, which sees the asm as writing it at issue, may copy it before then (it did: a loop phi move of
+  // the absmax2 register right behind the load).  Counters are uniform.
+  float2* const s_pair = reinterpret_cast<float2*>(smem + LDS_BYTES);
+  float* const s_c2 = reinterpret_cast<float*>(smem + LDS_BYTES + 2048);
+  const uint32_t* const s_land = reinterpret_cast<const uint32_t*>(smem + LDS_BYTES + 3072);
+  const uint32_t land0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(smem + LDS_BYTES + 3072)) + wave * 256;
+  long long sd_base = 0;
+  int sd_it = 0;
+  bool sd_pend = false;
+  float sd_off = 0.0f;
+  if constexpr (SIDE) {
+    // (before any DMA is issued: hipcc's vmcnt wait for the code2 load then waits for that load alone)
+    s_pair[tid] = side.fp4 ? make_float2(code4_value<FP4>(tid >> 4), code4_value<FP4>(tid & 15))
+                           : make_float2(code4_value<NF4>(tid >> 4), code4_value<NF4>(tid & 15));
+    if (side.nested) {
+      s_c2[tid] = side.code2[tid];
+      sd_off = *side.offset;
+    }
+    sd_base = (long long)blockIdx.x * side.per_wg;
+  }
+  // issue the next iteration's loads: packed dword -> slot row 0, statistic word -> 1 (q8 byte or fp32 absmax),
+  // absmax2 -> 2.  Only where nothing else holds M0 (after a k-tile's last A piece; the next SETB re-sets it).
+  auto side_issue = [&]() {
+    const long long gd = min(sd_base + (long long)sd_it * HG_THREADS + tid, side.ndw - 1);
+    const uint32_t blk = (uint32_t)((gd * 8) >> side.bs_shift);
+    if (side.mode & 4) {
+      ++sd_it;
+      sd_pend = true;
+      return;
+    }
+    if (side.mode & 1)
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1 nt"
+                   : : "v"((uint32_t)gd * 4u), "s"(side.packed), "s"(land0) : "memory");
+    else
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                   : : "v"((uint32_t)gd * 4u), "s"(side.packed), "s"(land0) : "memory");
+    if (side.nested) {
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %1"
+                   : : "v"(blk), "s"(side.q8), "s"(land0 + 1024) : "memory");
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                   : : "v"((blk >> side.bs2_shift) * 4u), "s"(side.absmax2), "s"(land0 + 2048) : "memory");
+    } else {
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                   : : "v"(blk * 4u), "s"(side.absmax), "s"(land0 + 1024) : "memory");
+    }
+    ++sd_it;
+    sd_pend = true;
+  };
+  // consume the pending iteration in three parts spread over MFMAs (after a wait covering its DMA): the landed words,
+  // then the statistic and the table lookups, then fp32 code * absmax, one RNE cast each, one 16-B store
+  uint32_t sd_w = 0, sd_q = 0, sd_a2 = 0;
+  float sd_am = 0.0f;
+  float2 sd_p[4];
+  auto side_words = [&]() {
+    sd_w = s_land[tid];
+    sd_q = s_land[256 + tid];
+    sd_a2 = s_land[512 + tid];
+  };
+  auto side_lookup = [&]() {
+    sd_am = side.nested ? __fadd_rn(__fmul_rn(s_c2[sd_q & 0xFF], __uint_as_float(sd_a2)), sd_off) : __uint_as_float(sd_q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sd_p[i] = s_pair[(sd_w >> (8 * i)) & 0xFF];
+  };
+  auto side_store = [&]() {
+    const long long gd = sd_base + (long long)(sd_it - 1) * HG_THREADS + tid;
+    hg_u32x4_t o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = cvt_pk<T16>(__fmul_rn(sd_p[i].x, sd_am), __fmul_rn(sd_p[i].y, sd_am));
+    // (s_nop 1: the store-data -> VALU overwrite wait state hipcc does not see through the asm)
+    if (gd < side.ndw && !(side.mode & 2)) {
+      if (side.mode & 1)
+        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" : : "v"((uint32_t)gd * 16u), "v"(o), "s"(side.out) : "memory");
+      else
+        asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"((uint32_t)gd * 16u), "v"(o), "s"(side.out) : "memory");
+    }
+    sd_pend = false;
+  };
 
   // ---- tile order: XCD-contiguous ids; groups of 4 M-tiles x all N-tiles (an XCD's 32 tiles share A / B rows)
   const int tilesN = (N + BN - 1) / BN, tilesM = (M + BM - 1) / BM;
@@ -445,11 +555,17 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   // the tile boundary; the fragment reads of a k-tile never share an MFMA gap with more than one DMA issue.  The
   // half-width tiles (64 MFMAs per k-tile, 12 pieces) follow the same order on the HgPlan3 positions below.
   using P3 = HgPlan3<WI, WJ>;
+  int sd_cd = 0;                                          // k-tiles until the next side step
   auto tile3 = [&](auto first, auto last, int t) {
     constexpr bool FIRST = decltype(first)::value, L = decltype(last)::value;
     constexpr int S = WI * WJ;                           // MFMAs per k32 step
     const int st = t & 1;
     const int kn = min(t + 2, nk - 1);
+    bool sd_go = false;                                  // side step in this k-tile (not the last: it has no B3)
+    if constexpr (SIDE && !L) {
+      sd_go = sd_cd == 0;
+      sd_cd = sd_go ? side.every - 1 : sd_cd - 1;
+    }
     // (unrolled at compile time -- hg_static_for hands the body a constant q: with a runtime loop of 2 S iterations
     // the unroller gave up on the 256 x 256 tile and left the accumulator and fragment arrays in scratch)
     hg_static_for<2 * S>([&](auto qc) {
@@ -475,6 +591,12 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
         if constexpr (q == P3::B3) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM) : "memory");
           __builtin_amdgcn_s_barrier();
+          if constexpr (SIDE) if (sd_go && sd_pend) side_words();      // its DMA is older than this tile's pieces
+        }
+        if constexpr (SIDE) {                            // (a few MFMAs between the dependent LDS reads)
+          if constexpr (q == P3::B3 + 4) if (sd_go && sd_pend) side_lookup();
+          if constexpr (q == P3::B3 + 10) if (sd_go && sd_pend) side_store();
+          if constexpr (q == P3::SIDEQ) if (sd_go && sd_it < side.iters) side_issue();
         }
         constexpr int r = P3::nread(q);                  // w0[0], x0[0..WI-1], w0[1..WJ-1]: the order of their use
         if constexpr (r == 0) w0[0] = rd(st ^ 1, wo0, 0);
@@ -505,6 +627,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
 #pragma unroll
     for (int i = 0; i < WJ; ++i) dma_b(k1, 1, i);
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(WI + WJ) : "memory");   // tile 0 landed; tile 1 in flight
+    if constexpr (SIDE) __builtin_amdgcn_s_waitcnt(0xC07F);          // (the side tables' LDS writes)
     __builtin_amdgcn_s_barrier();
   }
 #pragma unroll
@@ -533,6 +656,32 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (SIDE) {
+    // the pending side iteration (its loads are covered by the vmcnt(0) above) and the ones the loop had no room for
+    if (sd_pend) {
+      side_words();
+      side_lookup();
+      side_store();
+    }
+    for (; sd_it < side.iters; ++sd_it) {
+      const long long gd = sd_base + (long long)sd_it * HG_THREADS + tid;
+      if (gd >= side.ndw) continue;
+      const long long blk = (gd * 8) >> side.bs_shift;
+      const uint32_t w = reinterpret_cast<const uint32_t*>(side.packed)[gd];
+      const float am = side.nested ? __fadd_rn(__fmul_rn(s_c2[side.q8[blk]], side.absmax2[blk >> side.bs2_shift]), sd_off)
+                                   : side.absmax[blk];
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 p = s_pair[(w >> (8 * i)) & 0xFF];
+        v[2 * i] = __fmul_rn(p.x, am);
+        v[2 * i + 1] = __fmul_rn(p.y, am);
+      }
+      reinterpret_cast<uint4*>(side.out)[gd] =
+          make_uint4(cvt_pk<T16>(v[0], v[1]), cvt_pk<T16>(v[2], v[3]), cvt_pk<T16>(v[4], v[5]), cvt_pk<T16>(v[6], v[7]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
 
   // ---- epilogue: acc[j][i][r] = C[m0 + 128 wm + 16 i + fr][n0 + 128 wn + 16 j + 4 fg + r] -- four consecutive
   // columns of one row per accumulator: one 8-B store (16-bit outputs) or 16-B store (int32).  Full tiles (the common
@@ -728,42 +877,68 @@ long long hgemm_workspace_bytes(int m, int n, int k, int elem) {
   return pl.splits > 1 ? (long long)pl.splits * m * n * (long long)sizeof(float) : 0;
 }
 
-template <int OP, int V, int WI, int WJ>
-static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
-                               long long ldb, void* C, long long ldc, const float* rowStats, const float* colStats,
-                               const fp16_t* bias, float* ws) {
+// side: the next weight's dequantise to run inside this launch (nullptr: none); its per-workgroup share and step spacing
+// are set here from the grid
+template <int OP, int V, int WI, int WJ, bool SIDE>
+static void hgemm_launch_side(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
+                              long long ldb, void* C, long long ldc, const float* rowStats, const float* colStats,
+                              const fp16_t* bias, float* ws, const HgSide& sd) {
   const unsigned tiles = (unsigned)(((m + 32 * WI - 1) / (32 * WI)) * ((n + 32 * WJ - 1) / (32 * WJ)));
   if (pl.splits > 1) {
     if constexpr (OP == HG_BF16 || OP == HG_FP16)
-      hipLaunchKernelGGL((k_hgemm<OP, V, true, WI, WJ>), dim3(tiles * pl.splits), dim3(HG_THREADS), 0, current_stream(), m,
-                         n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, pl.splits, pl.kchunk);
+      hipLaunchKernelGGL((k_hgemm<OP, V, true, WI, WJ, SIDE>), dim3(tiles * pl.splits), dim3(HG_THREADS), 0,
+                         current_stream(), m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, pl.splits,
+                         pl.kchunk, sd);
   } else {
-    hipLaunchKernelGGL((k_hgemm<OP, V, false, WI, WJ>), dim3(tiles), dim3(HG_THREADS), 0, current_stream(), m, n, k, A,
-                       lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, pl.kchunk);
+    hipLaunchKernelGGL((k_hgemm<OP, V, false, WI, WJ, SIDE>), dim3(tiles), dim3(HG_THREADS), 0, current_stream(), m, n,
+                       k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, nullptr, 1, pl.kchunk, sd);
   }
+}
+
+template <int OP, int V, int WI, int WJ>
+static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
+                               long long ldb, void* C, long long ldc, const float* rowStats, const float* colStats,
+                               const fp16_t* bias, float* ws, const HgSide* side) {
+  if constexpr ((OP == HG_BF16 || OP == HG_FP16) && (V & 8192) != 0) {
+    if (side) {
+      const long long wgs = (long long)((m + 32 * WI - 1) / (32 * WI)) * ((n + 32 * WJ - 1) / (32 * WJ)) * pl.splits;
+      HgSide sd = *side;
+      sd.mode = g_side_mode;
+      const long long per = (sd.ndw + wgs - 1) / wgs;
+      sd.iters = (int)((per + HG_THREADS - 1) / HG_THREADS);
+      sd.per_wg = sd.iters * HG_THREADS;
+      // one side step every `every` k-tiles of the k-tiles that have a B3 (all but a workgroup's last)
+      const int steps = pl.kchunk - 1;
+      sd.every = steps > 0 ? std::max(1, (steps + sd.iters - 1) / sd.iters) : 1;
+      hgemm_launch_side<OP, V, WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sd);
+      return;
+    }
+  }
+  hgemm_launch_side<OP, V, WI, WJ, false>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, HgSide{});
 }
 
 template <int OP>
 int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* B, long long ldb, void* C, long long ldc,
                  const float* rowStats = nullptr, const float* colStats = nullptr, const fp16_t* bias = nullptr,
-                 float* ws = nullptr, long long ws_bytes = 0) {
+                 float* ws = nullptr, long long ws_bytes = 0, const HgSide* side = nullptr) {
   if (!hgemm_fits(m, n, k, lda, ldb, A, B, HgOpT<OP>::ELEM) || ldc < n) return 1;
   // the dequant epilogue reads 4 column scales / 4 bias halves per 16-B / 8-B load
   if (OP == HG_I8_DEQ && (((uintptr_t)colStats & 15) || ((uintptr_t)bias & 7))) return 1;
   constexpr bool FP = OP == HG_BF16 || OP == HG_FP16;
   // int8 (HG_I8_DEQ) and the round-3 schedule arm (chgemm_set_variant(1)) run the 256 x 256 tile only
   const bool full_only = !FP || g_hgemm_variant == 1;
+  if (side && (!FP || g_hgemm_variant == 1)) return 1;
   HgPlan pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, FP, full_only);
   if (pl.splits > 1 && (ws == nullptr || ((uintptr_t)ws & 15) ||
                         ws_bytes < (long long)pl.splits * m * n * (long long)sizeof(float)))
     pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, false, full_only);      // no (large enough) workspace: no split
   if (g_hgemm_variant == 1) {
-    hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
+    hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
   } else if (pl.wi == 8 && pl.wj == 8) {
-    hgemm_launch_shape<OP, HG_V, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
+    hgemm_launch_shape<OP, HG_V, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
   } else if constexpr (FP) {
-    if (pl.wi == 8) hgemm_launch_shape<OP, HG_V, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
-    else hgemm_launch_shape<OP, HG_V, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws);
+    if (pl.wi == 8) hgemm_launch_shape<OP, HG_V, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+    else hgemm_launch_shape<OP, HG_V, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
   }
   if constexpr (FP) {
     using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
@@ -817,16 +992,66 @@ int chgemm_tn_ws_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_
   BNB_RANGE("chgemm_tn_ws_fp16");
   return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
 }
+// [additive] chgemm_tn_ws_* that also dequantises the NEXT 4-bit weight inside the same launch (see HgSide): next_n
+// elements (% 8 == 0, below 2^31) of packed 4-bit `next_packed` (4-B aligned; fp4 = 1: FP4 code, else NF4) with fp32
+// block statistics `next_absmax` (next_q8 == NULL), or nested ones (next_q8 / next_code2 / next_absmax2 / next_offset,
+// blocksize2), into `next_out` (16-B aligned, the GEMM's element type) -- exactly cdequantize_blockwise_*_{nf4,fp4} /
+// the nested dequantise of that weight, run in the GEMM's shadow (the reference's dequantize_4bit of the following
+// layer, ref:python_src_quants/functional.py:1329).  Returns 0 = launched, 1 = not supported (nothing launched: run the
+// dequantise and the plain GEMM), 2 = launch error.
+static int hgemm_pf(int op, int m, int n, int k, const void* A, int lda, const void* W, int ldw, void* C, int ldc,
+                    float* ws, long long ws_bytes, const uint8_t* next_packed, const float* next_absmax,
+                    const uint8_t* next_q8, const float* next_code2, const float* next_absmax2, const float* next_offset,
+                    int fp4, int blocksize, int blocksize2, long long next_n, void* next_out) {
+  const bool nested = next_q8 != nullptr;
+  if (next_n <= 0 || next_n % 8 || next_n >= (1LL << 31) || !next_packed || !next_out || ((uintptr_t)next_packed & 3) ||
+      ((uintptr_t)next_out & 15) || blocksize < 8 || (blocksize & (blocksize - 1)))
+    return 1;
+  if (nested ? (!next_code2 || !next_absmax2 || !next_offset || blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1)))
+             : !next_absmax)
+    return 1;
+  bnb::HgSide sd{next_packed, next_absmax, next_q8, next_code2, next_absmax2, next_offset, next_out, next_n / 8,
+                 0, 0, 1, __builtin_ctz(blocksize), nested ? __builtin_ctz(blocksize2) : 0, nested ? 1 : 0, fp4 ? 1 : 0,
+                 0};
+  return op == bnb::HG_BF16
+             ? bnb::hgemm_launch<bnb::HG_BF16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes, &sd)
+             : bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes, &sd);
+}
+int chgemm_tn_pf_bf16(int m, int n, int k, const bf16_t* A, int lda, const bf16_t* W, int ldw, bf16_t* C, int ldc,
+                      float* ws, long long ws_bytes, const uint8_t* next_packed, const float* next_absmax,
+                      const uint8_t* next_q8, const float* next_code2, const float* next_absmax2,
+                      const float* next_offset, int fp4, int blocksize, int blocksize2, long long next_n,
+                      bf16_t* next_out) {
+  BNB_RANGE("chgemm_tn_pf_bf16");
+  return hgemm_pf(bnb::HG_BF16, m, n, k, A, lda, W, ldw, C, ldc, ws, ws_bytes, next_packed, next_absmax, next_q8,
+                  next_code2, next_absmax2, next_offset, fp4, blocksize, blocksize2, next_n, next_out);
+}
+int chgemm_tn_pf_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_t* W, int ldw, fp16_t* C, int ldc,
+                      float* ws, long long ws_bytes, const uint8_t* next_packed, const float* next_absmax,
+                      const uint8_t* next_q8, const float* next_code2, const float* next_absmax2,
+                      const float* next_offset, int fp4, int blocksize, int blocksize2, long long next_n,
+                      fp16_t* next_out) {
+  BNB_RANGE("chgemm_tn_pf_fp16");
+  return hgemm_pf(bnb::HG_FP16, m, n, k, A, lda, W, ldw, C, ldc, ws, ws_bytes, next_packed, next_absmax, next_q8,
+                  next_code2, next_absmax2, next_offset, fp4, blocksize, blocksize2, next_n, next_out);
+}
 long long chgemm_tn_workspace_bytes(int m, int n, int k) { return bnb::hgemm_workspace_bytes(m, n, k, 2); }
 // [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k) with enough workspace: out = {WI, WJ, splits,
 // k-tiles per split}; the output tile is 32 WI x 32 WJ (256 x 256, 256 x 128 or 128 x 256)
 void chgemm_tn_plan(int m, int n, int k, int* out) {
-  BNB_RANGE("chgemm_tn_workspace_bytes");
+  BNB_RANGE("chgemm_tn_plan");
   const bnb::HgPlan pl = bnb::hgemm_plan(m, n, k, 2, true, bnb::g_hgemm_variant == 1);
   out[0] = pl.wi;
   out[1] = pl.wj;
   out[2] = pl.splits;
   out[3] = pl.kchunk;
+}
+// [additive, testing] the side dequantise's A/B bits (HgSide::mode); returns the previous setting
+int chgemm_set_side_mode(int v) {
+  BNB_RANGE("chgemm_set_side_mode");
+  const int prev = bnb::g_side_mode;
+  bnb::g_side_mode = v;
+  return prev;
 }
 // [additive, testing] k_hgemm schedule: 0 = the default, 1 = the A/B arm (HG_V_ALT); returns the previous setting
 int chgemm_set_variant(int v) {

@@ -1013,9 +1013,64 @@ def _gemm_4bit_tokens(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, ab
     return rc == 0
 
 
+# Prefetched weights (gemm_4bit(..., prefetch=...)): per (device, dtype, stream) two weight slots and the slot + identity
+# of the weight the last prefetching GEMM dequantised into one of them.
+_PF_WS: dict = {}
+_PF_READY: dict = {}
+_PF_CUR: dict = {}          # the slot + identity the last consuming call read (reuse_weight chunks read it again)
+
+
+def _weight_meta(B: Tensor, state: QuantState, absmax: Optional[Tensor]) -> tuple:
+    """What identifies a dequantised weight: the packed bytes and the statistics (pointers and versions), shape,
+    blocksize and code -- the same tuple whether the weight is dequantised by its own call or prefetched."""
+    stats = absmax if absmax is not None else state.absmax
+    return (B.data_ptr(), B._version, stats.data_ptr(), stats._version, state.shape[0], state.shape[1], state.blocksize,
+            state.quant_type)
+
+
+def _pf_slots(key, device, dtype, numel: int) -> list:
+    slots = _PF_WS.get(key)
+    if slots is None or slots[0].numel() < numel:
+        slots = [torch.empty(numel, dtype=dtype, device=device) for _ in range(2)]
+        _PF_WS[key] = slots
+        _PF_READY.pop(key, None)
+        _PF_CUR.pop(key, None)
+    return slots
+
+
+def prefetched_weight(device, dtype=torch.bfloat16) -> Optional[tuple]:
+    """(slot, identity) of the weight waiting in a prefetch slot on this device / dtype / current stream, or None."""
+    return _PF_READY.get((torch.device(device), dtype, _stream_key(torch.device(device))))
+
+
+def _launch_prefetch_gemm(A2: Tensor, W: Tensor, out: Tensor, ws: Optional[Tensor], ws_bytes: int, pf: tuple,
+                          target: Tensor) -> int:
+    """chgemm_tn_pf_*: the GEMM of this call with the next weight's dequantise (pf = (B_next, state_next[, absmax]))
+    into `target` inside it.  Returns the C code (0 launched, 1 not supported -- nothing launched, 2 error)."""
+    Bn, sn = pf[0], pf[1]
+    an = pf[2] if len(pf) > 2 else None
+    rows, K = A2.shape
+    N = W.shape[0]
+    nested = an is None and sn.nested and _nested_stats_in_kernel_ok(sn)
+    if nested:
+        s2 = sn.state2
+        stats = [None, sn.absmax, s2.code, s2.absmax, _offset_on(sn, A2.device)]
+        bs2 = s2.blocksize
+    else:
+        stats = [an if an is not None else _absmax_fp32(sn), None, None, None, None]
+        bs2 = 0
+    Bc = Bn if Bn.is_contiguous() else Bn.contiguous()
+    is_on_gpu([Bc, target] + [t for t in stats if t is not None])
+    fn = lib.chgemm_tn_pf_bf16 if A2.dtype == torch.bfloat16 else lib.chgemm_tn_pf_fp16
+    return fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W), ct.c_int32(K),
+              get_ptr(out), ct.c_int32(N), get_ptr(ws), ct.c_longlong(ws_bytes), get_ptr(Bc),
+              *[get_ptr(t) for t in stats], ct.c_int32(1 if sn.quant_type == "fp4" else 0), ct.c_int32(sn.blocksize),
+              ct.c_int32(bs2), ct.c_longlong(sn.shape[0] * sn.shape[1]), get_ptr(target))
+
+
 def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = None,
               absmax: Optional[Tensor] = None, events: Optional[list] = None, reuse_weight: bool = False,
-              _route: Optional[str] = None) -> Tensor:
+              _route: Optional[str] = None, prefetch: Optional[tuple] = None) -> Tensor:
     """4-bit weight GEMM for any number of activation rows (the M>1 slot of cgemm_4bit_inference,
     ref:pythonInterface.cpp:377).  out[..., n] = A[..., :] @ W^T with W the dequantised [N, K] weight;
     replaces dequantize_4bit + F.linear (autograd/_functions.py:507).  Large problems (see
@@ -1026,7 +1081,12 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     the caller runs several row chunks of one product against the same, unmodified weight (the chunked
     sharded forward); on the library path the workspace still holding this weight's dequantisation
     from the previous call is used as is.  Prefill shapes on the library side of the static rule take the
-    measured route (GEMM_4BIT_ROUTE_TUNING); _route (one of GEMM_4BIT_ROUTES) forces one (internal)."""
+    measured route (GEMM_4BIT_ROUTE_TUNING); _route (one of GEMM_4BIT_ROUTES) forces one (internal).
+    prefetch = (B_next, state_next[, absmax_next]): the weight of the NEXT gemm_4bit call on this stream (the layer's
+    next projection, the next layer's first): on the dequantise + k_hgemm route its dequantise runs inside this call's
+    GEMM (chgemm_tn_pf_*, hgemm.hip HgSide) into a second weight slot, and the next call whose weight it is finds it
+    there and launches the GEMM alone -- the dequantise software-pipelined one weight ahead, the same bits as the
+    unpipelined pair.  On other routes the hint is ignored (the next call dequantises its own weight)."""
     if not gemm_4bit_supported(A, state):
         raise ValueError("gemm_4bit: needs bf16/fp16 activations and in_features % 64 == 0")
     N, K = state.shape[0], state.shape[1]
@@ -1089,12 +1149,23 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if ev:
         ev[0].record()
     if library:
-        W = _dequant_workspace(A.device, A.dtype, N * K).view(N, K)
         key = (A.device, A.dtype, _stream_key(A.device))
-        stats = absmax if absmax is not None else state.absmax
-        meta = (Bc.data_ptr(), Bc._version, stats.data_ptr(), stats._version, N, K, state.blocksize,
-                state.quant_type)
-        if not (reuse_weight and _DEQ_META.get(key) == meta):
+        meta = _weight_meta(Bc, state, absmax)
+        ready = _PF_READY.get(key)
+        cur_slot = None
+        if ready is not None and ready[1] == meta:
+            # dequantised by the previous call's GEMM (prefetch): consumed here (row chunks of this same product that
+            # follow with reuse_weight read it again, until a prefetch overwrites the slot)
+            cur_slot = ready[0]
+            del _PF_READY[key]
+            _PF_CUR[key] = ready
+        elif reuse_weight and _PF_CUR.get(key, (None, None))[1] == meta:
+            cur_slot = _PF_CUR[key][0]
+        if cur_slot is not None:
+            W = _PF_WS[key][cur_slot][:N * K].view(N, K)
+        else:
+            W = _dequant_workspace(A.device, A.dtype, N * K).view(N, K)
+        if cur_slot is None and not (reuse_weight and _DEQ_META.get(key) == meta):
             if absmax is None and not _dequant_4bit_nested(Bc, state, W):   # nested stats decoded in-kernel
                 absmax = _absmax_fp32(state)
             if absmax is not None:
@@ -1112,9 +1183,25 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
             # the hand-written GEMM (hgemm.hip); split-K over a workspace on small tile grids (chgemm_tn_ws_*)
             ws_bytes = int(lib.chgemm_tn_workspace_bytes(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K)))
             ws = _gemm_workspace(A.device, ws_bytes)
-            fn = lib.chgemm_tn_ws_bf16 if A.dtype == torch.bfloat16 else lib.chgemm_tn_ws_fp16
-            rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W),
-                    ct.c_int32(K), get_ptr(out), ct.c_int32(N), get_ptr(ws), ct.c_longlong(ws_bytes))
+            rc = 1
+            if prefetch is not None:
+                sn = prefetch[1]
+                nn = sn.shape[0] * sn.shape[1]
+                # (if the slots are re-made larger here, W still holds the old slot this call reads; both new ones
+                # are free)
+                slots = _pf_slots(key, A.device, A.dtype, max(nn, N * K))
+                target = 1 - cur_slot if cur_slot is not None else 0
+                rc = _launch_prefetch_gemm(A2, W, out, ws, ws_bytes, prefetch, slots[target][:nn])
+                if rc == 0:
+                    if _PF_CUR.get(key, (None,))[0] == target:
+                        _PF_CUR.pop(key, None)
+                    _PF_READY[key] = (target, _weight_meta(prefetch[0] if prefetch[0].is_contiguous()
+                                                           else prefetch[0].contiguous(), sn,
+                                                           prefetch[2] if len(prefetch) > 2 else None))
+            if rc == 1:
+                fn = lib.chgemm_tn_ws_bf16 if A.dtype == torch.bfloat16 else lib.chgemm_tn_ws_fp16
+                rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W),
+                        ct.c_int32(K), get_ptr(out), ct.c_int32(N), get_ptr(ws), ct.c_longlong(ws_bytes))
             post_call(prev_device)
             if rc:
                 raise RuntimeError(f"bitsandbytes HIP GEMM (chgemm_tn) returned {rc}: "

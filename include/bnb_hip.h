@@ -229,6 +229,23 @@ int chgemm_tn_ws_bf16(int m, int n, int k, const bnb_bf16* A, int lda, const bnb
 int chgemm_tn_ws_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp16* W, int ldw, bnb_fp16* C, int ldc,
                       float* ws, long long ws_bytes);
 long long chgemm_tn_workspace_bytes(int m, int n, int k);
+/* [additive] chgemm_tn_ws_* that also dequantises the NEXT 4-bit weight inside the same launch, software-pipelined one
+ * weight ahead (replaces the following call's cdequantize_blockwise_{bf16,fp16}_{nf4,fp4} / nested dequantise, i.e. the
+ * dequantize_4bit of ref:python_src_quants/functional.py:1329 before that layer's F.linear, autograd/_functions.py:507):
+ * next_n elements (% 8 == 0, < 2^31) of packed 4-bit next_packed (4-B aligned; fp4 = 1 FP4 code, 0 NF4) with fp32
+ * statistics next_absmax (next_q8 == NULL) or nested ones (next_q8, next_code2[256], next_absmax2, next_offset[1],
+ * blocksize2) into next_out (16-B aligned, the GEMM's element type); same bits as the dequantise kernel.  Returns 0 =
+ * launched, 1 = not supported (nothing launched), 2 = launch error. */
+int chgemm_tn_pf_bf16(int m, int n, int k, const bnb_bf16* A, int lda, const bnb_bf16* W, int ldw, bnb_bf16* C, int ldc,
+                      float* ws, long long ws_bytes, const unsigned char* next_packed, const float* next_absmax,
+                      const unsigned char* next_q8, const float* next_code2, const float* next_absmax2,
+                      const float* next_offset, int fp4, int blocksize, int blocksize2, long long next_n,
+                      bnb_bf16* next_out);
+int chgemm_tn_pf_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb_fp16* W, int ldw, bnb_fp16* C, int ldc,
+                      float* ws, long long ws_bytes, const unsigned char* next_packed, const float* next_absmax,
+                      const unsigned char* next_q8, const float* next_code2, const float* next_absmax2,
+                      const float* next_offset, int fp4, int blocksize, int blocksize2, long long next_n,
+                      bnb_fp16* next_out);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);
 /* [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k): out = {WI, WJ, splits, k-tiles per split};

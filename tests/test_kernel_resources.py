@@ -73,10 +73,13 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
     # per tile shape (WI, WJ): LDS-DMA pieces per k-tile and the vmcnt of barrier B3 (HgPlan3 in hgemm.hip)
     plans = {(8, 8): (16, 13), (8, 4): (12, 9), (4, 8): (12, 10)}
     shapes_seen = set()
+    side_seen = False
     for name, body in bodies:
         m = re.search(r"ELb[01]ELi(\d)ELi(\d)E", name)
         assert m, name
         shape = (int(m.group(1)), int(m.group(2)))
+        side = re.search(r"ELi\dELi\dELb1EE", name) is not None        # the side-dequantise (prefetch) form
+        sides = 0
         shapes_seen.add(shape)
         pieces, vm = plans[shape]
         lines = [ln.split(";")[0].strip() for ln in body.splitlines()]
@@ -89,15 +92,26 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
             if any(re.match(r"^\.LBB", ln) for ln in seg if ln.endswith(":")) and b - a > 4000:
                 continue                                         # first / last tile forms are separate code
             dma = sum(1 for ln in seg if ln.startswith("global_load_lds_dwordx4"))
-            other = [ln for ln in seg if vmem.match(ln) and not ln.startswith("global_load_lds_dwordx4")]
-            assert dma == pieces and not other, (name, dma, other[:3])
+            other = [i for i, ln in enumerate(seg) if vmem.match(ln) and not ln.startswith("global_load_lds_dwordx4")]
+            bars = [i for i, ln in enumerate(seg) if ln == "s_barrier"]
+            assert len(bars) >= 2, (name, bars)
+            if side:
+                # the side dequantise's loads / stores: only in the previous k-tile's tail, after its B3 and before this
+                # k-tile's B1 (so older than every piece the wait leaves in flight), and only the side's own kinds
+                assert all(bars[0] < i < bars[1] for i in other), (name, [seg[i] for i in other][:4])
+                assert all(re.match(r"global_(load_lds_dword |load_lds_ubyte |store_dwordx4 )", seg[i] + " ")
+                           for i in other), (name, [seg[i] for i in other][:4])
+                sides += bool(other)
+                other = []
+            assert dma == pieces and not other, (name, dma, [seg[i] for i in other][:3])
             counted += 1
             # of those 16: the previous k-tile's last 3 A pieces (after its barrier B3), then this k-tile's 13 (from its
             # barrier B1 on) before the wait -- the 13 the wait leaves in flight
-            bars = [i for i, ln in enumerate(seg) if ln == "s_barrier"]
-            assert len(bars) >= 2, (name, bars)
             before_b1 = sum(1 for ln in seg[:bars[1]] if ln.startswith("global_load_lds_dwordx4"))
             after_b1 = sum(1 for ln in seg[bars[1]:] if ln.startswith("global_load_lds_dwordx4"))
             assert (before_b1, after_b1) == (pieces - vm, vm), (name, before_b1, after_b1)
         assert counted >= 1, name
+        assert not side or sides >= 1, name          # (the side form's loop does hold side operations)
+        side_seen |= side
     assert shapes_seen == set(plans), shapes_seen
+    assert side_seen

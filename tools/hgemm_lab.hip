@@ -76,7 +76,8 @@ int main(int argc, char** argv) {
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   auto mine = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(tiles), dim3(HG_THREADS), 0, 0, M, N, K, (const void*)X, (long long)K, (const void*)W,
-                       (long long)K, (void*)Y1, (long long)N, nullptr, nullptr, nullptr, nullptr, 1, K * 2 / 128);
+                       (long long)K, (void*)Y1, (long long)N, nullptr, nullptr, nullptr, nullptr, 1, K * 2 / 128,
+                       bnb::HgSide{});
   };
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto timeit = [&](auto go, int R) {
