@@ -211,14 +211,14 @@ template <> struct HgPlan3<4, 8> {                      // 128 x 256: 8 B pieces
 // / dequantize_4bit_nested work of the following gemm_4bit call, software-pipelined one weight ahead so that the
 // HBM-bound dequantise runs in the MFMA-bound GEMM's shadow instead of as its own launch (the same values as
 // k_dequantize_4bit_stream, quant.hip: fp32 code * fp32 absmax, one RNE cast; nested statistics decoded as
-// code2[q8] * absmax2 + offset).  Workgroup w owns packed dwords [w * per_wg, (w + 1) * per_wg), 256 per "iteration"
-// (one dword = 8 weights per lane, coalesced).  In the main loop one iteration runs every `every` k-tiles, right after
+// code2[q8] * absmax2 + offset).  Workgroup w owns packed dwords [w * per_wg, (w + 1) * per_wg), 1024 per
+// "iteration" (4 dwords = 32 weights per lane, coalesced).  In the main loop one iteration runs every `every` k-tiles, right after
 // barrier B3: its loads are issued then and consumed one side step later, after that step's B3 wait -- the loads sit
 // before the next k-tile's DMA pieces, so vmcnt(VM) at the next B3 already covers them and the DMA counts stay exact
 // (the loads and the 16-B stores are inline asm, invisible to hipcc's wait insertion, like the DMA).  Iterations
 // left when the loop ends (few k-tiles) run after it.
 struct HgSide {
-  const uint8_t* packed;     // next weight, packed 4-bit (4-B aligned)
+  const uint8_t* packed;     // next weight, packed 4-bit (16-B aligned)
   const float* absmax;       // fp32 block statistics (nested == 0)
   const uint8_t* q8;         // nested: 8-bit codes of the statistics
   const float* code2;        // nested: their 256-entry code
@@ -227,8 +227,9 @@ struct HgSide {
   void* out;                 // ndw * 8 outputs of the GEMM's type (16-B aligned)
   long long ndw;             // packed dwords (elements / 8)
   int per_wg, iters, every, bs_shift, bs2_shift, nested, fp4;
-  int mode;                  // A/B bits (chgemm_set_side_mode): 1 = non-temporal side loads / stores, 2 = lab: no
-                             // side stores, 4 = lab: no side loads (timing only, wrong weights)
+  int mode;                  // A/B bits (chgemm_set_side_mode): 1 = non-temporal packed loads / output stores; lab
+                             // ablations (timing only, wrong weights): 2 = no side stores, 8 = no consumption, 16 = no
+                             // side loads, 32 = no side step in the loop, 64 = no tail
 };
 static int g_side_mode = 1;
 
@@ -257,24 +258,28 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   const int kt0 = split * kchunk;
   const uint8_t* A = reinterpret_cast<const uint8_t*>(Av) + (long long)kt0 * 128;
   const uint8_t* B = reinterpret_cast<const uint8_t*>(Bv) + (long long)kt0 * 128;
-  // side dequantise (SIDE): pair table (2 KiB) + code2 (1 KiB) + the LDS-DMA landing slots of one iteration's three
-  // words per lane ([3][256] u32)
-  constexpr int SIDE_LDS = SIDE ? 6144 : 0;
+  // side dequantise (SIDE): pair table (2 KiB) + code2 (1 KiB) + two buffers of LDS-DMA landing slots for one
+  // iteration (per wave: 64 x 16 B of packed weights, 64 x 4 B statistic codes, 64 x 4 B second-level scales)
+  constexpr int SIDE_WAVE = 1536, SIDE_BUF = 4 * SIDE_WAVE;
+  constexpr int SIDE_LDS = SIDE ? 3072 + 2 * SIDE_BUF : 0;
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + SIDE_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   using T16 = typename std::conditional<OP == HG_FP16, fp16_t, bf16_t>::type;
-  // Side dequantise state.  The iteration's words travel by LDS-DMA into the landing slots (global_load_lds_dword, M0 =
-  // the slot row of this wave), never into registers: an asm load's destination register is written when the load
-  // returns, and hipcc, which sees the asm as writing it at issue, may copy it before then (it did: a loop phi move of
-  // the absmax2 register right behind the load).  Counters are uniform.
+  // Side dequantise state.  One iteration = 4 packed dwords (32 weights, one statistics block) per lane, 1024 dwords
+  // per workgroup.  Its words travel by LDS-DMA into landing slots (global_load_lds_*, M0 = this wave's slot row),
+  // never into registers: an asm load's destination register is written when the load returns, and hipcc, which sees
+  // the asm as writing it at issue, may copy it before then (it did: a loop phi move of the absmax2 register right
+  // behind the load).  An iteration issued in k-tile t (after its last A piece, 3 loads) may stay in flight across B3
+  // of t+1 (that wait is vmcnt(VM + 3) then) and is consumed after B3 of t+2, whose wait covers it -- two k-tiles for
+  // loads that miss to HBM.  sd_i0 / i1 / i2: the iteration issued in this / the previous / the one-before k-tile (-1:
+  // none); landing buffer = iteration & 1.  Counters are uniform; dword indices fit 32 bits (host: ndw < 2^28).
   float2* const s_pair = reinterpret_cast<float2*>(smem + LDS_BYTES);
   float* const s_c2 = reinterpret_cast<float*>(smem + LDS_BYTES + 2048);
-  const uint32_t* const s_land = reinterpret_cast<const uint32_t*>(smem + LDS_BYTES + 3072);
-  const uint32_t land0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(smem + LDS_BYTES + 3072)) + wave * 256;
-  long long sd_base = 0;
-  int sd_it = 0;
-  bool sd_pend = false;
+  const uint8_t* const s_land = smem + LDS_BYTES + 3072 + wave * SIDE_WAVE;
+  const uint32_t land0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(smem + LDS_BYTES + 3072)) + wave * SIDE_WAVE;
+  uint32_t sd_base = 0;
+  int sd_it = 0, sd_i0 = -1, sd_i1 = -1, sd_i2 = -1;
   float sd_off = 0.0f;
   if constexpr (SIDE) {
     // (before any DMA is issued: hipcc's vmcnt wait for the code2 load then waits for that load alone)
@@ -284,64 +289,71 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       s_c2[tid] = side.code2[tid];
       sd_off = *side.offset;
     }
-    sd_base = (long long)blockIdx.x * side.per_wg;
+    sd_base = (uint32_t)blockIdx.x * (uint32_t)side.per_wg;
   }
-  // issue the next iteration's loads: packed dword -> slot row 0, statistic word -> 1 (q8 byte or fp32 absmax),
-  // absmax2 -> 2.  Only where nothing else holds M0 (after a k-tile's last A piece; the next SETB re-sets it).
+  // the lane's first dword of iteration `it` (clamped for the loads; the stores check the unclamped one)
+  auto side_gd = [&](int it) -> uint32_t { return sd_base + (uint32_t)it * 1024u + 4u * (uint32_t)tid; };
+  // issue the next iteration's loads, always exactly three (the B3 wait counts them): 16 B of packed weights -> row 0,
+  // statistic word -> row 1 (q8 byte or fp32 absmax), absmax2 -> row 2 (plain statistics: the absmax again).  Only
+  // where nothing else holds M0 (after a k-tile's last A piece; the next SETB re-sets it).
   auto side_issue = [&]() {
-    const long long gd = min(sd_base + (long long)sd_it * HG_THREADS + tid, side.ndw - 1);
-    const uint32_t blk = (uint32_t)((gd * 8) >> side.bs_shift);
-    if (side.mode & 4) {
-      ++sd_it;
-      sd_pend = true;
+    const uint32_t gd = min(side_gd(sd_it), (uint32_t)side.ndw - 4u);
+    const uint32_t blk = (gd * 8u) >> side.bs_shift;
+    const uint32_t lb = land0 + (sd_it & 1) * SIDE_BUF;
+    if (side.mode & 16) {                                // lab: no loads (the wait count is then wrong: timing only)
+      sd_i0 = sd_it++;
       return;
     }
     if (side.mode & 1)
-      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1 nt"
-                   : : "v"((uint32_t)gd * 4u), "s"(side.packed), "s"(land0) : "memory");
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt"
+                   : : "v"(gd * 4u), "s"(side.packed), "s"(lb) : "memory");
     else
-      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
-                   : : "v"((uint32_t)gd * 4u), "s"(side.packed), "s"(land0) : "memory");
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                   : : "v"(gd * 4u), "s"(side.packed), "s"(lb) : "memory");
     if (side.nested) {
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, %1"
-                   : : "v"(blk), "s"(side.q8), "s"(land0 + 1024) : "memory");
+                   : : "v"(blk), "s"(side.q8), "s"(lb + 1024) : "memory");
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
-                   : : "v"((blk >> side.bs2_shift) * 4u), "s"(side.absmax2), "s"(land0 + 2048) : "memory");
+                   : : "v"((blk >> side.bs2_shift) * 4u), "s"(side.absmax2), "s"(lb + 1280) : "memory");
     } else {
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
-                   : : "v"(blk * 4u), "s"(side.absmax), "s"(land0 + 1024) : "memory");
+                   : : "v"(blk * 4u), "s"(side.absmax), "s"(lb + 1024) : "memory");
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1"
+                   : : "v"(blk * 4u), "s"(side.absmax), "s"(lb + 1280) : "memory");
     }
-    ++sd_it;
-    sd_pend = true;
+    sd_i0 = sd_it++;
   };
-  // consume the pending iteration in three parts spread over MFMAs (after a wait covering its DMA): the landed words,
-  // then the statistic and the table lookups, then fp32 code * absmax, one RNE cast each, one 16-B store
-  uint32_t sd_w = 0, sd_q = 0, sd_a2 = 0;
+  // consume iteration `it` in parts spread over MFMAs (after a wait covering its DMA): the landed words; the statistic;
+  // then per packed dword j its 4 table lookups, and (a part later) fp32 code * absmax, one RNE cast each, one 16-B store
+  hg_u32x4_t sd_w = {0u, 0u, 0u, 0u};
+  uint32_t sd_q = 0, sd_a2 = 0;
   float sd_am = 0.0f;
   float2 sd_p[4];
-  auto side_words = [&]() {
-    sd_w = s_land[tid];
-    sd_q = s_land[256 + tid];
-    sd_a2 = s_land[512 + tid];
+  auto side_words = [&](int it) {
+    const uint8_t* l = s_land + (it & 1) * SIDE_BUF;
+    sd_w = *reinterpret_cast<const hg_u32x4_t*>(l + 16 * lane);
+    sd_q = *reinterpret_cast<const uint32_t*>(l + 1024 + 4 * lane);
+    sd_a2 = *reinterpret_cast<const uint32_t*>(l + 1280 + 4 * lane);
   };
-  auto side_lookup = [&]() {
+  auto side_stat = [&]() {
     sd_am = side.nested ? __fadd_rn(__fmul_rn(s_c2[sd_q & 0xFF], __uint_as_float(sd_a2)), sd_off) : __uint_as_float(sd_q);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sd_p[i] = s_pair[(sd_w >> (8 * i)) & 0xFF];
   };
-  auto side_store = [&]() {
-    const long long gd = sd_base + (long long)(sd_it - 1) * HG_THREADS + tid;
+  auto side_lookup = [&](int j) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sd_p[i] = s_pair[(sd_w[j] >> (8 * i)) & 0xFF];
+  };
+  auto side_store = [&](int it, int j) {
+    const uint32_t gd = side_gd(it) + (uint32_t)j;
     hg_u32x4_t o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = cvt_pk<T16>(__fmul_rn(sd_p[i].x, sd_am), __fmul_rn(sd_p[i].y, sd_am));
     // (s_nop 1: the store-data -> VALU overwrite wait state hipcc does not see through the asm)
-    if (gd < side.ndw && !(side.mode & 2)) {
+    if (gd < (uint32_t)side.ndw && !(side.mode & 2)) {
       if (side.mode & 1)
-        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" : : "v"((uint32_t)gd * 16u), "v"(o), "s"(side.out) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" : : "v"(gd * 16u), "v"(o), "s"(side.out) : "memory");
       else
-        asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"((uint32_t)gd * 16u), "v"(o), "s"(side.out) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" : : "v"(gd * 16u), "v"(o), "s"(side.out) : "memory");
     }
-    sd_pend = false;
   };
 
   // ---- tile order: XCD-contiguous ids; groups of 4 M-tiles x all N-tiles (an XCD's 32 tiles share A / B rows)
@@ -561,10 +573,15 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     constexpr int S = WI * WJ;                           // MFMAs per k32 step
     const int st = t & 1;
     const int kn = min(t + 2, nk - 1);
-    bool sd_go = false;                                  // side step in this k-tile (not the last: it has no B3)
-    if constexpr (SIDE && !L) {
-      sd_go = sd_cd == 0;
-      sd_cd = sd_go ? side.every - 1 : sd_cd - 1;
+    bool sd_go = false;                                  // side issue in this k-tile (not the last)
+    if constexpr (SIDE) {
+      sd_i2 = sd_i1;
+      sd_i1 = sd_i0;
+      sd_i0 = -1;
+      if constexpr (!L) {
+        sd_go = sd_cd == 0 && !(side.mode & 32);         // (mode 32, lab: no side step in the loop)
+        sd_cd = sd_go ? side.every - 1 : sd_cd - 1;
+      }
     }
     // (unrolled at compile time -- hg_static_for hands the body a constant q: with a runtime loop of 2 S iterations
     // the unroller gave up on the 256 x 256 tile and left the accumulator and fragment arrays in scratch)
@@ -589,13 +606,25 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
         if constexpr (q == P3::SETA) hg_set_m0(ldsA0 + st * STG);
         if constexpr (P3::apiece(q) >= 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[P3::apiece(q)]);
         if constexpr (q == P3::B3) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM) : "memory");
+          if (SIDE && sd_i1 >= 0) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM + 3) : "memory");  // (+ its 3 loads)
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM) : "memory");
           __builtin_amdgcn_s_barrier();
-          if constexpr (SIDE) if (sd_go && sd_pend) side_words();      // its DMA is older than this tile's pieces
-        }
-        if constexpr (SIDE) {                            // (a few MFMAs between the dependent LDS reads)
-          if constexpr (q == P3::B3 + 4) if (sd_go && sd_pend) side_lookup();
-          if constexpr (q == P3::B3 + 10) if (sd_go && sd_pend) side_store();
+          if constexpr (SIDE) if (sd_i2 >= 0 && !(side.mode & 8)) side_words(sd_i2);   // issued two k-tiles ago:
+        }                                                                                 // covered by this wait
+        if constexpr (SIDE) {                            // (3 MFMAs between the dependent LDS reads and their use)
+          constexpr int d = q - P3::B3;
+          if constexpr (d == 3) {
+            if (sd_i2 >= 0 && !(side.mode & 8)) {
+              side_stat();
+              side_lookup(0);
+            }
+          }
+          if constexpr (d == 6 || d == 9 || d == 12 || d == 15) {
+            if (sd_i2 >= 0 && !(side.mode & 8)) {
+              side_store(sd_i2, d / 3 - 2);
+              if constexpr (d < 15) side_lookup(d / 3 - 1);
+            }
+          }
           if constexpr (q == P3::SIDEQ) if (sd_go && sd_it < side.iters) side_issue();
         }
         constexpr int r = P3::nread(q);                  // w0[0], x0[0..WI-1], w0[1..WJ-1]: the order of their use
@@ -658,27 +687,37 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (SIDE) {
     // the pending side iteration (its loads are covered by the vmcnt(0) above) and the ones the loop had no room for
-    if (sd_pend) {
-      side_words();
-      side_lookup();
-      side_store();
-    }
-    for (; sd_it < side.iters; ++sd_it) {
-      const long long gd = sd_base + (long long)sd_it * HG_THREADS + tid;
-      if (gd >= side.ndw) continue;
-      const long long blk = (gd * 8) >> side.bs_shift;
-      const uint32_t w = reinterpret_cast<const uint32_t*>(side.packed)[gd];
+    // (the last k-tile shifted its predecessors' iterations into sd_i2 / sd_i1 and consumed neither)
+    auto consume = [&](int it) {
+      side_words(it);
+      side_stat();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        side_lookup(j);
+        side_store(it, j);
+      }
+    };
+    if (sd_i2 >= 0) consume(sd_i2);
+    if (sd_i1 >= 0) consume(sd_i1);
+    for (; sd_it < side.iters && !(side.mode & 64); ++sd_it) {     // (mode 64, lab: no tail)
+      const uint32_t gd0 = side_gd(sd_it);
+      if (gd0 >= (uint32_t)side.ndw) continue;
+      const uint32_t blk = (gd0 * 8u) >> side.bs_shift;
+      const hg_u32x4_t w = *reinterpret_cast<const hg_u32x4_t*>(side.packed + 4ull * gd0);
       const float am = side.nested ? __fadd_rn(__fmul_rn(s_c2[side.q8[blk]], side.absmax2[blk >> side.bs2_shift]), sd_off)
                                    : side.absmax[blk];
-      float v[8];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float2 p = s_pair[(w >> (8 * i)) & 0xFF];
-        v[2 * i] = __fmul_rn(p.x, am);
-        v[2 * i + 1] = __fmul_rn(p.y, am);
+      for (int j = 0; j < 4; ++j) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float2 p = s_pair[(w[j] >> (8 * i)) & 0xFF];
+          v[2 * i] = __fmul_rn(p.x, am);
+          v[2 * i + 1] = __fmul_rn(p.y, am);
+        }
+        reinterpret_cast<uint4*>(side.out)[gd0 + j] =
+            make_uint4(cvt_pk<T16>(v[0], v[1]), cvt_pk<T16>(v[2], v[3]), cvt_pk<T16>(v[4], v[5]), cvt_pk<T16>(v[6], v[7]));
       }
-      reinterpret_cast<uint4*>(side.out)[gd] =
-          make_uint4(cvt_pk<T16>(v[0], v[1]), cvt_pk<T16>(v[2], v[3]), cvt_pk<T16>(v[4], v[5]), cvt_pk<T16>(v[6], v[7]));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -905,8 +944,8 @@ static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void
       HgSide sd = *side;
       sd.mode = g_side_mode;
       const long long per = (sd.ndw + wgs - 1) / wgs;
-      sd.iters = (int)((per + HG_THREADS - 1) / HG_THREADS);
-      sd.per_wg = sd.iters * HG_THREADS;
+      sd.iters = (int)((per + 4 * HG_THREADS - 1) / (4 * HG_THREADS));   // 4 dwords per lane per iteration
+      sd.per_wg = sd.iters * 4 * HG_THREADS;
       // one side step every `every` k-tiles of the k-tiles that have a B3 (all but a workgroup's last)
       const int steps = pl.kchunk - 1;
       sd.every = steps > 0 ? std::max(1, (steps + sd.iters - 1) / sd.iters) : 1;
@@ -993,7 +1032,7 @@ int chgemm_tn_ws_fp16(int m, int n, int k, const fp16_t* A, int lda, const fp16_
   return bnb::hgemm_launch<bnb::HG_FP16>(m, n, k, A, lda, W, ldw, C, ldc, nullptr, nullptr, nullptr, ws, ws_bytes);
 }
 // [additive] chgemm_tn_ws_* that also dequantises the NEXT 4-bit weight inside the same launch (see HgSide): next_n
-// elements (% 8 == 0, below 2^31) of packed 4-bit `next_packed` (4-B aligned; fp4 = 1: FP4 code, else NF4) with fp32
+// elements (% 32 == 0, below 2^31) of packed 4-bit `next_packed` (16-B aligned; fp4 = 1: FP4 code, else NF4) with fp32
 // block statistics `next_absmax` (next_q8 == NULL), or nested ones (next_q8 / next_code2 / next_absmax2 / next_offset,
 // blocksize2), into `next_out` (16-B aligned, the GEMM's element type) -- exactly cdequantize_blockwise_*_{nf4,fp4} /
 // the nested dequantise of that weight, run in the GEMM's shadow (the reference's dequantize_4bit of the following
@@ -1004,8 +1043,9 @@ static int hgemm_pf(int op, int m, int n, int k, const void* A, int lda, const v
                     const uint8_t* next_q8, const float* next_code2, const float* next_absmax2, const float* next_offset,
                     int fp4, int blocksize, int blocksize2, long long next_n, void* next_out) {
   const bool nested = next_q8 != nullptr;
-  if (next_n <= 0 || next_n % 8 || next_n >= (1LL << 31) || !next_packed || !next_out || ((uintptr_t)next_packed & 3) ||
-      ((uintptr_t)next_out & 15) || blocksize < 8 || (blocksize & (blocksize - 1)))
+  // (whole 32-weight groups, 16-B aligned operands, statistics blocks of >= 32: each lane's 4 packed dwords share one)
+  if (next_n <= 0 || next_n % 32 || next_n >= (1LL << 31) || !next_packed || !next_out || ((uintptr_t)next_packed & 15) ||
+      ((uintptr_t)next_out & 15) || blocksize < 32 || (blocksize & (blocksize - 1)))
     return 1;
   if (nested ? (!next_code2 || !next_absmax2 || !next_offset || blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1)))
              : !next_absmax)

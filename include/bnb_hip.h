@@ -232,7 +232,7 @@ long long chgemm_tn_workspace_bytes(int m, int n, int k);
 /* [additive] chgemm_tn_ws_* that also dequantises the NEXT 4-bit weight inside the same launch, software-pipelined one
  * weight ahead (replaces the following call's cdequantize_blockwise_{bf16,fp16}_{nf4,fp4} / nested dequantise, i.e. the
  * dequantize_4bit of ref:python_src_quants/functional.py:1329 before that layer's F.linear, autograd/_functions.py:507):
- * next_n elements (% 8 == 0, < 2^31) of packed 4-bit next_packed (4-B aligned; fp4 = 1 FP4 code, 0 NF4) with fp32
+ * next_n elements (% 32 == 0, < 2^31) of packed 4-bit next_packed (16-B aligned; fp4 = 1 FP4 code, 0 NF4) with fp32
  * statistics next_absmax (next_q8 == NULL) or nested ones (next_q8, next_code2[256], next_absmax2, next_offset[1],
  * blocksize2) into next_out (16-B aligned, the GEMM's element type); same bits as the dequantise kernel.  Returns 0 =
  * launched, 1 = not supported (nothing launched), 2 = launch error. */

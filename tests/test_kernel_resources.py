@@ -83,7 +83,11 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
         shapes_seen.add(shape)
         pieces, vm = plans[shape]
         lines = [ln.split(";")[0].strip() for ln in body.splitlines()]
-        waits = [i for i, ln in enumerate(lines) if ln == f"s_waitcnt vmcnt({vm})"]
+        # (the side form waits vmcnt(VM + 3) instead when the previous k-tile issued side loads: they may stay in flight)
+        # (the prologue's wait for tile 0, vmcnt(WI + WJ), comes before the first barrier: not a B3 wait)
+        first_bar = lines.index("s_barrier")
+        waits = [i for i, ln in enumerate(lines) if i > first_bar and
+                 (ln == f"s_waitcnt vmcnt({vm})" or (side and ln == f"s_waitcnt vmcnt({vm + 3})"))]
         assert len(waits) >= 2, (name, len(waits))
         # the steady-state loop body: consecutive waits inside one basic-block chain (the loop) hold 16 pieces
         counted = 0
@@ -91,24 +95,36 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
             seg = lines[a + 1:b]
             if any(re.match(r"^\.LBB", ln) for ln in seg if ln.endswith(":")) and b - a > 4000:
                 continue                                         # first / last tile forms are separate code
-            dma = sum(1 for ln in seg if ln.startswith("global_load_lds_dwordx4"))
-            other = [i for i, ln in enumerate(seg) if vmem.match(ln) and not ln.startswith("global_load_lds_dwordx4")]
+            if side and b - a < 16 and not any(vmem.match(ln) for ln in seg):
+                continue                                         # the two arms of one B3 wait
+            # (the side dequantise's 16-B packed-weight load is one asm statement "s_mov_b32 m0, sN; s_nop 0; load";
+            # the GEMM's pieces in the loop are chained "load; s_add_u32 m0, m0, imm")
+            code = [j for j, ln in enumerate(seg) if ln]
+
+            def side_x4(i):
+                k = code.index(i)
+                return k >= 2 and seg[code[k - 1]] == "s_nop 0" and seg[code[k - 2]].startswith("s_mov_b32 m0")
+            dma = sum(1 for i, ln in enumerate(seg) if ln.startswith("global_load_lds_dwordx4") and not side_x4(i))
+            other = [i for i, ln in enumerate(seg) if vmem.match(ln) and
+                     (not ln.startswith("global_load_lds_dwordx4") or side_x4(i))]
             bars = [i for i, ln in enumerate(seg) if ln == "s_barrier"]
             assert len(bars) >= 2, (name, bars)
             if side:
                 # the side dequantise's loads / stores: only in the previous k-tile's tail, after its B3 and before this
                 # k-tile's B1 (so older than every piece the wait leaves in flight), and only the side's own kinds
                 assert all(bars[0] < i < bars[1] for i in other), (name, [seg[i] for i in other][:4])
-                assert all(re.match(r"global_(load_lds_dword |load_lds_ubyte |store_dwordx4 )", seg[i] + " ")
-                           for i in other), (name, [seg[i] for i in other][:4])
+                assert all(re.match(r"global_(load_lds_dword |load_lds_dwordx4 |load_lds_ubyte |store_dwordx4 )",
+                                    seg[i] + " ") for i in other), (name, [seg[i] for i in other][:4])
                 sides += bool(other)
                 other = []
             assert dma == pieces and not other, (name, dma, [seg[i] for i in other][:3])
             counted += 1
             # of those 16: the previous k-tile's last 3 A pieces (after its barrier B3), then this k-tile's 13 (from its
             # barrier B1 on) before the wait -- the 13 the wait leaves in flight
-            before_b1 = sum(1 for ln in seg[:bars[1]] if ln.startswith("global_load_lds_dwordx4"))
-            after_b1 = sum(1 for ln in seg[bars[1]:] if ln.startswith("global_load_lds_dwordx4"))
+            before_b1 = sum(1 for i, ln in enumerate(seg[:bars[1]]) if ln.startswith("global_load_lds_dwordx4")
+                            and not side_x4(i))
+            after_b1 = sum(1 for i, ln in enumerate(seg) if i >= bars[1] and ln.startswith("global_load_lds_dwordx4")
+                           and not side_x4(i))
             assert (before_b1, after_b1) == (pieces - vm, vm), (name, before_b1, after_b1)
         assert counted >= 1, name
         assert not side or sides >= 1, name          # (the side form's loop does hold side operations)

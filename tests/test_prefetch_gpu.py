@@ -104,16 +104,17 @@ def test_prefetch_tail_and_edges(dtype, case):
 
 
 def test_prefetch_declines_unsupported():
-    """A next weight the side path does not take (element count % 8) launches nothing and says so (1)."""
+    """A next weight the side path does not take (element count % 32: each lane moves 32 weights) launches nothing and
+    says so (1)."""
     dtype = torch.bfloat16
     X = torch.randn(256, 1024, device="cuda").to(dtype)
     W = torch.randn(1024, 1024, device="cuda").to(dtype)
-    q2, s2 = _weight(8, 9, dtype, "nf4", False, 3)           # 72 elements: fine
+    q2, s2 = _weight(8, 12, dtype, "nf4", False, 3)          # 96 elements: fine
     out, nxt = _pf_gemm(X, W, (q2, s2))
     torch.cuda.synchronize()
     assert torch.equal(nxt, F.dequantize_4bit(q2, s2).view_as(nxt))
-    q3, s3 = _weight(3, 6, dtype, "nf4", False, 3)           # 18 elements: not a whole dword
-    target = torch.empty(18, device="cuda", dtype=dtype)
+    q3, s3 = _weight(3, 8, dtype, "nf4", False, 3)           # 24 elements: not a whole 32-weight group
+    target = torch.empty(24, device="cuda", dtype=dtype)
     rc = F._launch_prefetch_gemm(X, W, torch.empty(256, 1024, device="cuda", dtype=dtype), None, 0, (q3, s3), target)
     assert rc == 1
 

@@ -1,6 +1,6 @@
 """A/B of the side dequantise inside k_hgemm (chgemm_tn_pf_bf16) at the metric shape: the plain GEMM, the dequantise
 kernel alone, their sum, and the prefetching GEMM under each chgemm_set_side_mode setting (1 = non-temporal side loads
-/ stores, 2 = no side stores, 4 = no side loads: lab ablations, wrong weights).  Interleaved rounds after a clock ramp."""
+/ stores, 2 = no side stores, lab ablation, the weight is not written).  Interleaved rounds after a clock ramp."""
 import ctypes as ct
 import os
 import sys
@@ -14,7 +14,7 @@ import python_src_quants.functional as F  # noqa: E402
 from python_src_quants.cextension import lib  # noqa: E402
 
 M, N, K = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (4096, 4096, 11008)))
-modes = [int(a) for a in os.environ.get("SIDE_MODES", "0,1,3,5,7").split(",")]
+modes = [int(a) for a in os.environ.get("SIDE_MODES", "1,3,9,17,33,97").split(",")]
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(1)
 X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
