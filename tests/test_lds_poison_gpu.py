@@ -5,7 +5,8 @@ must return bit for bit what it returns without the poison.  A read of a staged 
 vmcnt / barrier count one short), a slot that a short last group never writes, or a wrong M0 destination would read
 the poison and change the result (round 3 dropped a GEMV variant that returned NaN this way).
 Kernels covered: k_hgemm (bf16 / fp16, split-K, int8 4-wave), igemm_256 (8-wave), the whole-K few-token kernel, the
-split-K few-token kernel, the decode GEMVs (balanced / dot / wide / multi-row), the fused NF4 GEMM and the dequantise."""
+split-K few-token kernel, the decode GEMVs (balanced / dot / wide / multi-row), the fused NF4 GEMM, the dequantise and
+k_hgemm with the side dequantise of the next weight (prefetch)."""
 import ctypes as ct
 
 import pytest
@@ -139,3 +140,30 @@ def test_fused_and_dequant_under_poison(dev, poison_visible, rows, N, K):
     out = torch.empty(rows, N, device=dev, dtype=torch.bfloat16)
     _same_under_poison(F, dev, lambda: F.gemm_4bit(X, q, st, out=out, _route="fused"))
     _same_under_poison(F, dev, lambda: F.dequantize_4bit(q, st))
+
+
+@pytest.mark.parametrize("mnk,nxt", [((300, 260, 192), (1003, 192)), ((4096, 1024, 8192), (11008, 4096)),
+                                     ((1000, 1100, 4096), (64, 64))])
+@pytest.mark.parametrize("nested", [True, False])
+def test_prefetch_side_dequant_under_poison(dev, poison_visible, mnk, nxt, nested):
+    """k_hgemm with the next weight's dequantise inside it (its landing slots, pair table and code2 copy in LDS): the
+    GEMM output and the written weight must not change under the poison."""
+    F = _F()
+    m, n, k = mnk
+    g = torch.Generator(device=dev).manual_seed(m + k)
+    X = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    W = (torch.rand(n, k, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    Wn = (torch.randn(*nxt, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    q, st = F.quantize_4bit(Wn, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    out = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    target = torch.empty(nxt[0] * nxt[1], device=dev, dtype=torch.bfloat16)
+    nbytes = int(F.lib.chgemm_tn_workspace_bytes(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k)))
+    ws = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=dev)
+
+    def run():
+        F.pre_call(dev)
+        assert F._launch_prefetch_gemm(X, W, out, ws, nbytes, (q, st), target) == 0
+        return torch.cat([out.view(-1), target])
+    _same_under_poison(F, dev, run)
+    torch.cuda.synchronize()
+    assert torch.equal(target, F.dequantize_4bit(q, st).view(-1))
