@@ -17,6 +17,8 @@
 // 16-B vector stores: it is HBM-bound (roofline: 0.5 B in + 2 B out per bf16 element).
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace bnb {
 
 // ============================================================================ quantize
@@ -393,21 +395,32 @@ void quantize_blockwise(const float* code, const T* A, float* absmax, uint8_t* o
   BNB_LAUNCH_CHECK("quantize_blockwise");
 }
 
+// Launch shape of k_dequantize_4bit_stream (A/B knob cdequantize_set_stream_cfg): dwords per lane per pass (4, 8 or 16)
+// and a cap on the grid (0: one pass per workgroup; else at most that many workgroups, grid-stride passes)
+static int g_dq_p = 8, g_dq_grid_cap = 0;
+template <typename T, int DT, bool NESTED>
+static void launch_dq_stream(const uint8_t* A, const float* absmax, T* out, int bs_shift, long long ndw,
+                             const NestedStats& ns) {
+  auto go = [&](auto pc) {
+    constexpr int P = decltype(pc)::value;
+    long long wgs = (ndw + 256 * P - 1) / (256 * P);
+    if (wgs > 65536) wgs = 65536;
+    if (g_dq_grid_cap > 0 && wgs > g_dq_grid_cap) wgs = g_dq_grid_cap;
+    hipLaunchKernelGGL((k_dequantize_4bit_stream<T, DT, P, NESTED>), dim3((int)wgs), dim3(256), 0, current_stream(), A,
+                       absmax, out, bs_shift, ndw, ns);
+  };
+  if (g_dq_p == 4) go(std::integral_constant<int, 4>{});
+  else if (g_dq_p == 16) go(std::integral_constant<int, 16>{});
+  else go(std::integral_constant<int, 8>{});
+}
+
 template <typename T, int DT>
 void dequantize_blockwise(const float* code, const uint8_t* A, const float* absmax, T* out, int blocksize, long long n) {
   if (n <= 0) return;
   if (blocksize < 64 || (blocksize & (blocksize - 1))) { set_error(1, "dequantize_blockwise: unsupported blocksize"); return; }
   if constexpr (DT != GENERAL8BIT && sizeof(T) == 2) {
     if (n % 8 == 0 && ((uintptr_t)A & 3) == 0 && aligned16(out)) {
-#ifndef BNB_DQ_P
-#define BNB_DQ_P 8
-#endif
-      constexpr int P = BNB_DQ_P;
-      const long long ndw = n / 8;
-      const long long wgs = (ndw + 256 * P - 1) / (256 * P);
-      const int grid = (int)(wgs < 65536 ? wgs : 65536);
-      hipLaunchKernelGGL((k_dequantize_4bit_stream<T, DT, P>), dim3(grid), dim3(256), 0, current_stream(), A, absmax,
-                         out, __builtin_ctz(blocksize), ndw);
+      launch_dq_stream<T, DT, false>(A, absmax, out, __builtin_ctz(blocksize), n / 8, NestedStats{});
       BNB_LAUNCH_CHECK("dequantize_blockwise");
       return;
     }
@@ -430,13 +443,8 @@ bool dequantize_4bit_nested(const uint8_t* A, const uint8_t* q8, const float* co
   if (blocksize < 64 || (blocksize & (blocksize - 1)) || blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1)) ||
       n % 8 != 0 || ((uintptr_t)A & 3) != 0 || !aligned16(out))
     return false;
-  constexpr int P = BNB_DQ_P;
-  const long long ndw = n / 8;
-  const long long wgs = (ndw + 256 * P - 1) / (256 * P);
-  const int grid = (int)(wgs < 65536 ? wgs : 65536);
   const NestedStats ns{q8, code2, absmax2, offset, __builtin_ctz(blocksize2)};
-  hipLaunchKernelGGL((k_dequantize_4bit_stream<T, DT, P, true>), dim3(grid), dim3(256), 0, current_stream(), A,
-                     nullptr, out, __builtin_ctz(blocksize), ndw, ns);
+  launch_dq_stream<T, DT, true>(A, nullptr, out, __builtin_ctz(blocksize), n / 8, ns);
   BNB_LAUNCH_CHECK("dequantize_4bit_nested");
   return true;
 }
@@ -477,6 +485,15 @@ using namespace bnb;
 
 // ============================================================================ C-ABI
 extern "C" {
+
+// [additive, testing] k_dequantize_4bit_stream launch shape: p = packed dwords per lane per pass (4, 8, 16), grid_cap =
+// at most this many workgroups (0: none); returns the previous p
+int cdequantize_set_stream_cfg(int p, int grid_cap) {
+  const int prev = g_dq_p;
+  g_dq_p = p;
+  g_dq_grid_cap = grid_cap;
+  return prev;
+}
 
 #define BNB_QUANT_ABI(fname, T, DT)                                                                   \
   void fname(float* code, T* A, float* absmax, unsigned char* out, int blocksize, const int n) {     \

@@ -391,16 +391,24 @@ class ShardedDecode:
                  dtype=torch.bfloat16, device=None, gather: str = "rccl", rank: Optional[int] = None):
         self.local_fn, self.world, self.group = local_fn, world, group
         self.x = torch.zeros(1, in_features, dtype=dtype, device=device)
-        self.y = torch.empty(1, n_local, dtype=dtype, device=device)
         self.gathered = torch.empty(world, 1, n_local, dtype=dtype, device=device)
-        self.rows = torch.empty(1, world * n_local, dtype=dtype, device=device)
         self.graph = None
         # gather="ipc": the one-shot peer-memory all-gather (IpcAllGather) instead of RCCL's all_gather_into_tensor
         self.ipc = None
         if gather == "ipc":
             r = dist.get_rank(group) if rank is None else rank
             self.ipc = IpcAllGather(n_local, world, r, group, self.x.device, dtype)
-        elif gather != "rccl":
+            self.y = torch.empty(1, n_local, dtype=dtype, device=device)
+            self.rows = torch.empty(1, world * n_local, dtype=dtype, device=device)
+        elif gather == "rccl":
+            # At M = 1 the gathered [world, 1, n] IS the assembled [1, world * n] row in memory, and this rank's slice
+            # of it can be the GEMV's output: the GEMV writes straight into place, the all-gather runs in place
+            # (send buffer = receive buffer + rank * n), and nothing is copied -- one kernel per step at world 1
+            # (round 3 had the GEMV + two copies).
+            r = (dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0) if rank is None else rank
+            self.y = self.gathered[r]
+            self.rows = self.gathered.view(1, world * n_local)
+        else:
             raise ValueError(f"ShardedDecode: unknown gather {gather!r}")
 
     def set_input(self, x: torch.Tensor):
@@ -411,10 +419,11 @@ class ShardedDecode:
         self.local_fn(self.x, self.y)
         if self.ipc is not None:
             return self.ipc(self.y, self.rows)
-        gather_columns(self.y, self.world, self.group, out=self.gathered)
-        if not _collective(self.world):
-            self.gathered[0].copy_(self.y)
-        self.rows.view(1, self.world, -1).copy_(self.gathered.permute(1, 0, 2))
+        if _collective(self.world):
+            if dist.get_backend(self.group) == "gloo":
+                dist.all_gather(list(self.gathered.unbind(0)), self.y.clone(), group=self.group)
+            else:
+                dist.all_gather_into_tensor(self.gathered, self.y, group=self.group)   # in place
         return self.rows
 
     def capture(self, warmup: int = 2) -> bool:

@@ -246,6 +246,11 @@ int chgemm_tn_pf_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb
                       const unsigned char* next_q8, const float* next_code2, const float* next_absmax2,
                       const float* next_offset, int fp4, int blocksize, int blocksize2, long long next_n,
                       bnb_fp16* next_out);
+/* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
+ * grid_cap = at most that many workgroups (0 = none); returns the previous p */
+int cdequantize_set_stream_cfg(int p, int grid_cap);
+/* [additive, testing] k_hgemm side-dequantise A/B bits (chgemm_tn_pf_*); returns the previous value */
+int chgemm_set_side_mode(int v);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);
 /* [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k): out = {WI, WJ, splits, k-tiles per split};
