@@ -137,6 +137,26 @@ __device__ __forceinline__ void hg_set_m0(uint32_t lds) { asm volatile("s_mov_b3
 
 __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r >> 1) & 7)) << 4); }
 
+// one dword per lane by LDS-DMA (lane l -> lds + 4 l), scalar base + 32-bit lane offset, M0 written here
+__device__ __forceinline__ void glds4_sv_m0(const void* sbase, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" : : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+
+// mm_dequant of two adjacent outputs of one row on packed fp32 (v_pk_mul_f32 / v_pk_add_f32: each lane's two
+// elements rounded exactly as mm_dequant_value's scalar ops -- same operation order, one RNE per op), then one packed
+// RNE cast to fp16: {fp16(lo), fp16(hi)}
+__device__ __forceinline__ uint32_t mm_dequant_pair(int32_t a0, int32_t a1, float rs, float cs0, float cs1, float b0,
+                                                    float b1) {
+  hg_f32x2_t v = {(float)a0, (float)a1};
+  v = v * (hg_f32x2_t){6.200012e-05f, 6.200012e-05f};
+  v = v * (hg_f32x2_t){rs, rs};
+  v = v * (hg_f32x2_t){cs0, cs1};
+  asm volatile("" : "+v"(v));                          // (no fma / fma_mix folding across the barriers)
+  v = v + (hg_f32x2_t){b0, b1};
+  asm volatile("" : "+v"(v));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, hg_f16x2_t));
+}
+
 // V: schedule variant bits (A/B arms of tools/hgemm_lab.hip; HG_V is the launched one):
 //   1 = step-1 fragment reads all after half 1's MFMAs, 2 = no sched_barrier fences in half 2,
 //   4 = next-step fragments read in MFMA-need order, 8 = DMA spread (8 pieces before the wait, 8 after, one per
@@ -262,7 +282,10 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   // iteration (per wave: 64 x 16 B of packed weights, 64 x 4 B statistic codes, 64 x 4 B second-level scales)
   constexpr int SIDE_WAVE = 1536, SIDE_BUF = 4 * SIDE_WAVE;
   constexpr int SIDE_LDS = SIDE ? 3072 + 2 * SIDE_BUF : 0;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + SIDE_LDS];
+  // HG_I8_DEQ: the tile's row scales (BM floats), column scales (BN floats) and bias (BN halves), brought in by LDS-DMA
+  // in the prologue so that the epilogue reads them from LDS instead of waiting on global loads
+  constexpr int STATS_LDS = (OP == HG_I8_DEQ) ? 4 * BM + 4 * BN + 2 * BN : 0;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + SIDE_LDS + STATS_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   using T16 = typename std::conditional<OP == HG_FP16, fp16_t, bf16_t>::type;
@@ -646,6 +669,18 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     for (int q = 0; q < 16; ++q) rs_load(min(1, nk - 1), q);
     __syncthreads();
   } else {
+    if constexpr (OP == HG_I8_DEQ) {
+      // the statistics first (older than tile 0's pieces: the prologue's vmcnt below covers them); lanes past the
+      // matrix edge fetch the last row / column (those slots are read only by the edge path, which does not use them)
+      const uint32_t sb = lds_base + LDS_BYTES + SIDE_LDS;
+      for (int c = wave; c < BM / 64; c += 4)
+        glds4_sv_m0(rowStats, 4u * (uint32_t)min(m0 + 64 * c + lane, M - 1), sb + 256 * c);
+      for (int c = wave; c < BN / 64; c += 4)
+        glds4_sv_m0(colStats, 4u * (uint32_t)min(n0 + 64 * c + lane, N - 1), sb + 4 * BM + 256 * c);
+      if (bias != nullptr && (N & 1) == 0)                 // bias as fp16 pairs (whole dwords: N even)
+        for (int c = wave; c < BN / 128; c += 4)
+          glds4_sv_m0(bias, 4u * (uint32_t)min(n0 / 2 + 64 * c + lane, N / 2 - 1), sb + 4 * BM + 4 * BN + 256 * c);
+    }
 #pragma unroll
     for (int i = 0; i < WI; ++i) dma_a(0, 0, i);
 #pragma unroll
@@ -767,16 +802,22 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     // HG_I8_DEQ: the lane's row / column statistics and bias loaded once, up front (the fragment registers are free
     // now): 8 row scales, 8 x 4 column scales (16-B loads: nb % 4 == 0) and 8 x 4 bias halves.  Loading them per
     // accumulator (256 dependent L1 loads per lane) cost ~24 us of fixed epilogue per launch.
+    // (round 4: from the LDS copy the prologue's DMA made, not from global memory at this point)
     float rsv[WI];
     f32x4_t csv[WJ];
     uint2 bsv[WJ];
     if constexpr (OP == HG_I8_DEQ) {
+      const uint8_t* sst = smem + LDS_BYTES + SIDE_LDS;
+      const int rl = 16 * WI * wm + (lane_e & 15), cl = 16 * WJ * wn + 4 * (lane_e >> 4);
 #pragma unroll
-      for (int i = 0; i < WI; ++i) rsv[i] = rowStats[mb + 16 * i];
+      for (int i = 0; i < WI; ++i) rsv[i] = *reinterpret_cast<const float*>(sst + 4 * (rl + 16 * i));
 #pragma unroll
       for (int j = 0; j < WJ; ++j) {
-        csv[j] = *reinterpret_cast<const f32x4_t*>(colStats + nb + 16 * j);
-        bsv[j] = bias ? *reinterpret_cast<const uint2*>(bias + nb + 16 * j) : make_uint2(0u, 0u);
+        csv[j] = *reinterpret_cast<const f32x4_t*>(sst + 4 * BM + 4 * (cl + 16 * j));
+        if ((N & 1) == 0)
+          bsv[j] = bias ? *reinterpret_cast<const uint2*>(sst + 4 * BM + 4 * BN + 2 * (cl + 16 * j)) : make_uint2(0u, 0u);
+        else
+          bsv[j] = bias ? *reinterpret_cast<const uint2*>(bias + nb + 16 * j) : make_uint2(0u, 0u);
       }
     }
 #pragma unroll
@@ -789,14 +830,9 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
           v.x = cvt_pk<T>(acc[j][i][0], acc[j][i][1]);
           v.y = cvt_pk<T>(acc[j][i][2], acc[j][i][3]);
         } else if constexpr (OP == HG_I8_DEQ) {
-          uint16_t h[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint16_t bh = (uint16_t)((r < 2 ? bsv[j].x : bsv[j].y) >> (16 * (r & 1)));
-            h[r] = __builtin_bit_cast(uint16_t, mm_dequant_value(acc[j][i][r], rsv[i], csv[j][r],
-                                                                 (float)__builtin_bit_cast(fp16_t, bh)));
-          }
-          v = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+          auto bf = [&](uint32_t w, int hi) { return (float)__builtin_bit_cast(fp16_t, (uint16_t)(w >> (16 * hi))); };
+          v.x = mm_dequant_pair(acc[j][i][0], acc[j][i][1], rsv[i], csv[j][0], csv[j][1], bf(bsv[j].x, 0), bf(bsv[j].x, 1));
+          v.y = mm_dequant_pair(acc[j][i][2], acc[j][i][3], rsv[i], csv[j][2], csv[j][3], bf(bsv[j].y, 0), bf(bsv[j].y, 1));
         }
         *reinterpret_cast<uint2*>(ep + (16 * i + (lane_e & 15)) * EPI_PITCH + 2 * (16 * j + 4 * (lane_e >> 4))) = v;
         __builtin_amdgcn_sched_barrier(0);   // one accumulator at a time: no VGPR burst that displaces AGPRs
