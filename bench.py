@@ -240,8 +240,10 @@ def bench_decode_sharded(dev, world, rank, steps, warmup, gather="rccl"):
            "weight_bytes_per_rank": wbytes, "rank_weight_gbs": wbytes / per / 1e9,
            "step": "gemv_4bit on this rank's rows" + (
                " + one-shot peer-memory all-gather (IpcAllGather, one kernel) into the [1, N] row" if gather == "ipc"
-               else " + RCCL all_gather_into_tensor [1, N/g] + [1, N] assembly" if world > 1 else " + [1, N] copy"),
-           "note": "host wall per replayed step (barrier-bracketed, max over ranks): the latency a decode token pays"}
+               else " written into its slice of the [1, N] row + in-place RCCL all_gather_into_tensor" if world > 1
+               else " written straight into the [1, N] row (one kernel)"),
+           "note": "host wall per replayed step (barrier-bracketed, max over ranks): the latency a decode token pays "
+                   "for this one layer, including the graph launch"}
     dec.set_input(x_check)
     res["_row"] = dec().clone()
     torch.cuda.synchronize()
@@ -250,6 +252,66 @@ def bench_decode_sharded(dev, world, rank, steps, warmup, gather="rccl"):
         res["ipc_memory"] = dec.ipc.memory_kind
         dec.graph = None
         dec.ipc.close()
+    # The same step for `layers` distinct layers (own weight copies and buffers) captured in ONE graph, as a model's
+    # per-token graph holds all its layers: the per-layer latency without one graph launch per layer.  Every layer gets
+    # the same input, so every layer's row must equal the single step's bit for bit.
+    if graph:
+        from python_src_quants.parallel import ShardedDecode
+        layers = 8
+
+        def make(qw):
+            fn = lambda x, y: F.gemv_4bit(x, qw.t(), out=y, state=lin.quant_state)  # noqa: E731
+            return ShardedDecode(fn, lin.in_features, lin.end - lin.start, world, None, torch.bfloat16, dev,
+                                 gather=gather, rank=rank)
+        decs = [make(lin.qweight.clone()) for _ in range(layers)]
+        for d in decs:
+            d.set_input(x_check)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                for d in decs:
+                    d.step()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        gl, ok = torch.cuda.CUDAGraph(), 1
+        try:
+            with torch.cuda.graph(gl):
+                for d in decs:
+                    d.step()
+        except Exception:  # noqa: BLE001 - capture refused: no multi-layer number
+            ok = 0
+        if world > 1:
+            t = torch.tensor([ok], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = int(t.item())
+        if ok:
+            for _ in range(max(warmup, 3)):
+                gl.replay()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                gl.replay()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([el], device=dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = t.item()
+            res["us_per_layer_in_graph"] = el / steps / layers * 1e6
+            res["layers_per_graph"] = layers
+            res["layers_match_single_step_bitwise"] = all(torch.equal(d.rows, res["_row"]) for d in decs)
+        del gl
+        for d in decs:
+            if d.ipc is not None:
+                res["ipc_timeouts"] = res.get("ipc_timeouts", 0) + d.ipc.timeouts()
+                d.ipc.close()
     return res
 
 
