@@ -247,8 +247,12 @@ k_skinny_reduce(const float* __restrict__ ws, int nsplit, int M, int N, T* __res
     }
     const long long t = i0 / N, n = i0 - t * N;
     T* dst = out + t * ldc + n;
-    dst[0] = Io<T>::from_f32(s.x); dst[1] = Io<T>::from_f32(s.y);
-    dst[2] = Io<T>::from_f32(s.z); dst[3] = Io<T>::from_f32(s.w);
+    if ((((uintptr_t)dst) & 7) == 0) {                 // one 8-B store of the four (one RNE cast each)
+      *reinterpret_cast<uint2*>(dst) = make_uint2(sk_cvt2v<T>((f32x2_t){s.x, s.y}), sk_cvt2v<T>((f32x2_t){s.z, s.w}));
+    } else {
+      dst[0] = Io<T>::from_f32(s.x); dst[1] = Io<T>::from_f32(s.y);
+      dst[2] = Io<T>::from_f32(s.z); dst[3] = Io<T>::from_f32(s.w);
+    }
   } else {
     for (long long i = i0; i < i0 + 4 && i < mn; ++i) {
       float s = ws[i];
@@ -311,7 +315,7 @@ long long skinny_workspace_bytes(int m, int n, int k) {
   if (n < 1 || n > SK_MAX_TOKENS || k < 128 || k % 128) return 0;
   const int mt = skinny_tiles(n), nb = mt == 1 ? skinny_nb<1>() : (mt == 2 ? skinny_nb<2>() : skinny_nb<4>());
   const int s = (k / 128 + nb - 1) / nb;
-  return s > 1 ? (long long)s * n * m * (long long)sizeof(float) : 0;
+  return std::max(s > 1 ? (long long)s * n * m * (long long)sizeof(float) : 0LL, t64_workspace_bytes(m, n, k));
 }
 
 // m = out features (weight rows), n = tokens, k = in features.  False: not applicable (shape, alignment
@@ -320,7 +324,11 @@ template <typename T>
 bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
                              int blocksize, int blocksize2, const float* code, T* out, int ldc, float* ws,
                              long long ws_bytes) {
-  // the whole-K MFMA kernel first (gemm4bit_fewtok.hip), unless a lab / test knob selects one of the older kernels
+  // 33..64 tokens: the split-K tile kernel that shares the token rows across 192 weight rows (gemm4bit_t64.hip); then
+  // the whole-K MFMA kernel (gemm4bit_fewtok.hip), unless a lab / test knob selects one of the older kernels
+  if (g_fewtoken_kernel == 0 && g_skinny_cfg < 0 &&
+      launch_gemm_4bit_t64<T>(m, n, k, A, lda, B, ldb, st, blocksize, blocksize2, code, out, ldc, ws, ws_bytes))
+    return true;
   if (g_fewtoken_kernel == 0 && g_skinny_cfg < 0 &&
       launch_gemm_4bit_fewtok<T>(m, n, k, A, lda, B, ldb, st, blocksize, blocksize2, code, out, ldc))
     return true;

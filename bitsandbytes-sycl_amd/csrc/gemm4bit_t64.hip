@@ -1,0 +1,440 @@
+// 33..64-token 4-bit weight GEMM (batched decode / short prefill) for gfx950: the M > 1 slot of cgemm_4bit_inference
+// (ref:sycl/pythonInterface.cpp:377-378), i.e. dequantize_4bit + F.linear (ref:python_src_quants/autograd/
+// _functions.py:491-507), in the arithmetic of the whole-K few-token kernel (gemm4bit_fewtok.hip; the reference GEMV's
+// T-precision code values, ref:sycl/sycl_code/kernel_gemm.cpp:1291-1294): each weight enters the MFMA as T(code[q]),
+// a 64-element block's two MFMAs sum T(code) x products in fp32, and the block sum is scaled by its fp32 absmax (one
+// fma per output).  Tolerance class: the GEMV's.
+//
+// Why a separate kernel from 33 tokens on (round 4; the split-K weight stream k_gemm_4bit_skinny ran 11008 x 4096 at
+// 64 tokens in 25.9 us + a 6.6 us reduce, 0.10 of HBM): per CU the traffic of a tile of R weight rows x Kc in-features
+// x 64 tokens is 64 Kc x 2 B of tokens (from L2) + R Kc / 2 B of weights + R x 64 x 4 B of fp32 partials per split;
+// for the whole product that is N K (128 / R + 512 / Kc) bytes beside the weights, least near R ~ 4 Kc / 16.  The
+// skinny kernel runs 64 rows x 384 k (3.3 B of side traffic per weight), the whole-K kernel 48 rows x K (2.8 B, and
+// its token fragments for 64 tokens do not fit the registers); here 192 rows x K / 4 at 11008 x 4096 (0.9 B).
+//
+// Geometry: 4 waves, each 48 weight rows (3 groups of 16) x all 64 tokens (4 MFMA tiles) x the workgroup's K range
+// (whole 4-block groups of 256 k; split-K over workgroups, fp32 partials summed in split order by k_skinny_reduce).
+// Every operand arrives by LDS-DMA, so the k-loop holds no VGPR-destination load and every wait is an explicit count:
+//   tokens   shared by the 4 waves: 2 slots x 16 KiB ([64 tokens][128 k], 16-B slots XOR-swizzled by token row & 15:
+//            the A-operand reads of 16 rows at one k are conflict-free), 16 pieces per 2-block half-group, 4 per wave;
+//   weights  per wave: 2 slots x 6 KiB (48 rows x 128 B of one 4-block group, slots swizzled by (row >> 1) & 7 as in
+//            the whole-K kernel), 6 pieces per group;
+//   stats    per wave: 2 slots; plain: the row's 4 block absmax (16 B), nested: its 4 codes (dword) + absmax2;
+//   table    {T(code[hi]), T(code[lo])} per packed byte, 32 bank-private copies (the whole-K kernel's layout, one
+//            v_perm_b32 per lookup address), the nested code map in the rows' spare halves.
+// Per 4-block group g (half-groups 2g, 2g + 1): wait for half-group h's tokens (vmcnt: the pieces issued since -- the
+// next half-group's tokens and the next group's weights -- may fly) + barrier; consume its 2 blocks; barrier (every
+// wave is done with that token slot); refill the slot with half-group h + 2.  After the second half the wave's
+// weight slot is refilled with group g + 2.  Past the last group the refills re-load the last one into slots nobody
+// reads (constant counts, no branches); vmcnt(0) before the end.
+#include "gemm_common.hpp"
+#include "gemv_common.hpp"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace bnb {
+
+constexpr int T64_RG = 3, T64_WAVES = 4, T64_THREADS = 64 * T64_WAVES;
+constexpr int T64_ROWS = 16 * T64_RG * T64_WAVES;            // 192 weight rows per workgroup
+constexpr int T64_TABLE = 256 * 256;
+constexpr int T64_TOK = 64 * 256;                            // one token slot: 64 tokens x 128 k
+constexpr int T64_WGRP = 16 * T64_RG * 128;                  // one weight slot per wave: 48 rows x 128 B
+constexpr int T64_STAT = 1024;                               // one statistics slot per wave
+constexpr int T64_OFF_TOK = T64_TABLE;
+constexpr int T64_OFF_W = T64_OFF_TOK + 2 * T64_TOK;
+constexpr int T64_OFF_S = T64_OFF_W + T64_WAVES * 2 * T64_WGRP;
+constexpr int T64_LDS = T64_OFF_S + T64_WAVES * 2 * T64_STAT;   // 150 KiB
+constexpr int T64_WPIECES = 16 * T64_RG / 8;                 // 6 weight pieces per wave per group
+constexpr int T64_TPIECES = 4;                               // token pieces per wave per half-group
+
+template <typename T> struct T64Mfma;
+template <> struct T64Mfma<bf16_t> {
+  __device__ static __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                   0, 0, 0);
+  }
+};
+template <> struct T64Mfma<fp16_t> {
+  __device__ static __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                  0, 0);
+  }
+};
+
+// LDS-DMA, scalar base + 32-bit lane offset, M0 = the destination (written here; this kernel uses M0 for nothing else)
+template <int BYTES>
+__device__ __forceinline__ void t64_dma(const void* sbase, uint32_t voff, uint32_t lds) {
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" : : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+template <int BYTES>
+__device__ __forceinline__ void t64_dma_nt(const void* sbase, uint32_t voff, uint32_t lds) {
+  static_assert(BYTES == 16, "16-B pieces");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+
+// N = out features (weight rows), M = tokens (1..64), K = in features (% 256 == 0), blocksize 64.  Workgroup
+// (row tile rt, split sp): rows rt * 192 .., groups [sp * kc, min((sp + 1) * kc, K / 256)).  ksplit > 1: fp32
+// partials ws[sp][token][row]; else the outputs.
+// ABL (lab ablations, timing only): 1 = no vmcnt waits, 2 = no token DMA after the prologue, 4 = no weight DMA after
+// the prologue, 8 = no MFMAs, 16 = no table lookups, 32 = no output / partial stores, 64 = no table build, 128 = no
+// barriers in the loop, 256 = no token fragment reads
+template <typename T, bool NESTED, int ABL = 0>
+__global__ void __launch_bounds__(T64_THREADS, 1)
+k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
+                SkStats st, const float* __restrict__ code, T* __restrict__ out, int ldc, float* __restrict__ ws,
+                int ksplit, int kc) {
+  constexpr int WOPS = (NESTED ? 2 : 1) + T64_WPIECES;       // VMEM instructions of one weight-group issue
+  constexpr int TOPS = T64_TPIECES;                          // ... of one token half-group issue
+  __shared__ __attribute__((aligned(16))) uint8_t sm[T64_LDS];
+  uint8_t* table = sm;
+  auto code2s_at = [&](uint32_t t) -> const float& {
+    return *reinterpret_cast<const float*>(table + 256 * (t >> 5) + 128 + 4 * (t & 31));
+  };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, g = lane >> 4;
+  const int bid = blockIdx.x, rt = bid / ksplit, sp = bid - rt * ksplit;
+  const int r0 = rt * T64_ROWS + wave * 16 * T64_RG;         // this wave's first weight row
+  const int ngr = K >> 8, gr0 = sp * kc, ng = min(kc, ngr - gr0);   // this workgroup's groups (>= 1, host rule)
+
+  // ---- the pair table (and the nested code map) before any DMA is in flight: hipcc's waits for these loads then wait
+  // for these loads alone.  Code values by scalar loads, selected per entry.
+  if constexpr ((ABL & 64) == 0) {
+    float dt[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dt[j] = code[j];
+    float hi = dt[0], lo = dt[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      hi = (tid >> 4) == j ? dt[j] : hi;
+      lo = (tid & 15) == j ? dt[j] : lo;
+    }
+    const uint32_t v = Dot2<T>::pair(hi, lo);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * tid + 16 * ((k + tid) & 7)) = make_uint4(v, v, v, v);
+    if constexpr (NESTED) *reinterpret_cast<float*>(table + 256 * (tid >> 5) + 128 + 4 * (tid & 31)) = st.code2[tid];
+  }
+  float offset = 0.0f;
+  if constexpr (NESTED) offset = *st.offset;
+  __builtin_amdgcn_s_waitcnt(0);                             // (table values in place before the stream starts)
+
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)sm);
+  // token pieces: this wave's pieces q = 4 wave + i of a half-group slot; lane l -> token row t = 4 q + (l >> 4),
+  // physical 16-B slot p = l & 15 holding logical slot p ^ (t & 15) (k = 8 x logical slot within the 128 k)
+  uint32_t toff[T64_TPIECES];
+#pragma unroll
+  for (int i = 0; i < T64_TPIECES; ++i) {
+    const int q = 4 * wave + i, t = 4 * q + (lane >> 4), p = lane & 15;
+    toff[i] = (uint32_t)min(t, M - 1) * (uint32_t)lda * 2u + 16u * (uint32_t)(p ^ (t & 15));
+  }
+  // weight pieces: piece j = rows 8 j .. 8 j + 7 of the wave's 48; lane l -> row 8 j + (l >> 3), LDS slot l & 7 holding
+  // source slot (l & 7) ^ ((row >> 1) & 7)
+  uint32_t woff[T64_WPIECES];
+#pragma unroll
+  for (int j = 0; j < T64_WPIECES; ++j) {
+    const int rr = 8 * j + (lane >> 3);
+    woff[j] = (uint32_t)min(r0 + rr, N - 1) * (uint32_t)ldb + 16u * (uint32_t)((lane & 7) ^ ((rr >> 1) & 7));
+  }
+  // statistics: lane l -> the wave's row min(l, 47); its first block index (bs = 64: 2 ldb row / 64)
+  const uint32_t sblk0 = (uint32_t)((2LL * ldb * min(r0 + min(lane, 16 * T64_RG - 1), N - 1)) >> 6);
+  const uint32_t tok_lds = lds0 + T64_OFF_TOK;
+  const uint32_t w_lds = lds0 + T64_OFF_W + wave * 2 * T64_WGRP;
+  const uint32_t s_lds = lds0 + T64_OFF_S + wave * 2 * T64_STAT;
+
+  auto issue_w = [&](int gi, int slot) {                     // weight group gi (clamped) -> this wave's slot
+    if constexpr ((ABL & 4) != 0) if (gi >= 2) return;
+    const int G = gr0 + min(gi, ng - 1);
+    const uint32_t j0 = sblk0 + 4u * (uint32_t)G;
+    if constexpr (NESTED) {
+      t64_dma<4>(st.q8, j0, s_lds + slot * T64_STAT);
+      t64_dma<4>(st.absmax2, 4u * (j0 >> st.bs2_shift), s_lds + slot * T64_STAT + 256);
+    } else {
+      t64_dma<16>(st.absmax, 4u * j0, s_lds + slot * T64_STAT);
+    }
+    const uint8_t* src = B + 128LL * G;
+#pragma unroll
+    for (int j = 0; j < T64_WPIECES; ++j) t64_dma_nt<16>(src, woff[j], w_lds + slot * T64_WGRP + 1024 * j);
+  };
+  auto issue_t = [&](int hi, int slot) {                     // token half-group hi (clamped) -> token slot
+    if constexpr ((ABL & 2) != 0) if (hi >= 2) return;
+    const int h = min(hi, 2 * ng - 1);
+    const T* src = A + 64LL * (4 * gr0 + 2 * h);             // k0 = 64 x (first block of the half-group)
+#pragma unroll
+    for (int i = 0; i < T64_TPIECES; ++i) t64_dma<16>(src, toff[i], tok_lds + slot * T64_TOK + 1024 * (4 * wave + i));
+  };
+
+  f32x4_t acc[T64_RG][4];
+#pragma unroll
+  for (int rg = 0; rg < T64_RG; ++rg)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[rg][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint32_t lane4 = (uint32_t)(lane & 31) * 4;
+
+  // consume the 2 blocks of half-group `half` (0 / 1) of group gi: tokens from token slot `half`, weights and statistics
+  // from slot gi & 1
+  auto consume = [&](int gi, int half) {
+    // One wave per SIMD: nothing else hides an LDS round trip, so every read of the half-group is issued before any
+    // is used -- token fragments of both blocks, the weight words and statistics of all row groups, then all table
+    // lookups -- and only then the 48 MFMAs (one basic block; hipcc waits on lgkmcnt just before each first use).
+    const int ws_slot = gi & 1;
+    const uint8_t* tk = sm + T64_OFF_TOK + half * T64_TOK;
+    const uint8_t* wr = sm + T64_OFF_W + (wave * 2 + ws_slot) * T64_WGRP;
+    const uint8_t* sr = sm + T64_OFF_S + (wave * 2 + ws_slot) * T64_STAT;
+    uint2 wv[2][T64_RG];
+    uint32_t q4[T64_RG];
+    float a2[T64_RG], a[2][T64_RG];
+#pragma unroll
+    for (int rg = 0; rg < T64_RG; ++rg) {
+      const int rr = 16 * rg + n;
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2) {
+        const int slot16 = (2 * (2 * half + b2) + (g >> 1)) ^ ((rr >> 1) & 7);
+        wv[b2][rg] = *reinterpret_cast<const uint2*>(wr + rr * 128 + 16 * slot16 + 8 * (g & 1));
+      }
+      if constexpr (NESTED) {
+        q4[rg] = *reinterpret_cast<const uint32_t*>(sr + 4 * rr);
+        a2[rg] = *reinterpret_cast<const float*>(sr + 256 + 4 * rr);
+      } else {
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2) a[b2][rg] = *reinterpret_cast<const float*>(sr + 16 * rr + 4 * (2 * half + b2));
+      }
+    }
+    uint4 xf[2][4][2];                                       // tokens: A tile mt, lane (t = n, g): row 16 mt + n
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int ls = 8 * b2 + 2 * g + s;                 // logical 16-B slot: k 64 b2 + 16 g + 8 s
+          if constexpr ((ABL & 256) != 0) xf[b2][mt][s] = make_uint4(ls, mt, n, 0);
+          else xf[b2][mt][s] = *reinterpret_cast<const uint4*>(tk + (16 * mt + n) * 256 + 16 * (ls ^ n));
+        }
+    if constexpr (NESTED) {
+#pragma unroll
+      for (int rg = 0; rg < T64_RG; ++rg)
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2)
+          a[b2][rg] = __fadd_rn(__fmul_rn(code2s_at((q4[rg] >> (8 * (2 * half + b2))) & 0xFF), a2[rg]), offset);
+    }
+    uint4 bf[2][T64_RG][2];                                  // weight operands: byte i of the word -> entry, lane copy
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+      for (int rg = 0; rg < T64_RG; ++rg)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const uint32_t d = s ? wv[b2][rg].y : wv[b2][rg].x;
+          uint32_t l[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if constexpr ((ABL & 16) != 0) l[i] = d + i;
+            else l[i] = *reinterpret_cast<const uint32_t*>(table + __builtin_amdgcn_perm(d, lane4, 0x0C0C0000u | ((4u + i) << 8)));
+          }
+          bf[b2][rg][s] = make_uint4(l[0], l[1], l[2], l[3]);
+        }
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+      for (int rg = 0; rg < T64_RG; ++rg) {
+        f32x4_t blk[4];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            if constexpr ((ABL & 8) != 0) {
+              const f32x4_t z = s ? blk[mt] : f32x4_t{0.f, 0.f, 0.f, 0.f};
+              blk[mt] = z + f32x4_t{__uint_as_float(xf[b2][mt][s].x ^ bf[b2][rg][s].x), 0.f, 0.f, 0.f};
+            } else {
+              blk[mt] = T64Mfma<T>::mma(xf[b2][mt][s], bf[b2][rg][s], s ? blk[mt] : f32x4_t{0.f, 0.f, 0.f, 0.f});
+            }
+          }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[rg][mt][i] = __builtin_fmaf(a[b2][rg], blk[mt][i], acc[rg][mt][i]);
+      }
+  };
+
+  // ---- prologue: W(0), T(0), T(1), W(1) -- the steady state's order (at each wait the ops younger than the awaited
+  // token half-group are exactly the next half-group's tokens and one weight group)
+  issue_w(0, 0);
+  issue_t(0, 0);
+  issue_t(1, 1);
+  issue_w(1, 1);
+  for (int gi = 0; gi < ng; ++gi) {
+    if constexpr ((ABL & 1) == 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(TOPS + WOPS) : "memory");   // T(2 gi) and W(gi) landed (this wave)
+    if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();                                          // ... every wave's token pieces
+    __builtin_amdgcn_sched_barrier(0);
+    consume(gi, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                    // lgkmcnt(0): this wave's reads are done
+    if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();                                          // ... every wave's: token slot 0 is free
+    __builtin_amdgcn_sched_barrier(0);
+    issue_t(2 * gi + 2, 0);
+    if constexpr ((ABL & 1) == 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(TOPS + WOPS) : "memory");   // T(2 gi + 1) landed
+    if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    consume(gi, 1);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();                                          // token slot 1 and this wave's weight slot
+    __builtin_amdgcn_sched_barrier(0);                                     // are free
+    issue_t(2 * gi + 3, 1);
+    issue_w(gi + 2, gi & 1);
+  }
+  wait_vmcnt0();                                                           // no LDS-DMA may outlive the workgroup
+
+  // ---- outputs: acc[rg][mt][i] = token 16 mt + 4 g + i, weight row r0 + 16 rg + n (ABL 32: stored only where the
+  // value is an impossible one -- the computation stays live, the stores go).  A whole tile (64 tokens, 192 rows in
+  // range) stores unpredicated from a wave-uniform base per (token tile, i) plus one 32-bit lane offset; edge tiles
+  // check every element.
+  const bool whole = M == 64 && rt * T64_ROWS + T64_ROWS <= N;
+  if (whole && (ABL & 32) == 0) {
+    const uint32_t loff = (uint32_t)(4 * g) * (uint32_t)N + (uint32_t)(r0 + n);
+    if (ksplit > 1) {
+      float* wsb = ws + (long long)sp * 64 * N;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float* p = wsb + (long long)(16 * mt + i) * N;
+#pragma unroll
+          for (int rg = 0; rg < T64_RG; ++rg) p[loff + 16 * rg] = acc[rg][mt][i];
+        }
+    } else {
+      const uint32_t loo = (uint32_t)(4 * g) * (uint32_t)ldc + (uint32_t)(r0 + n);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          T* p = out + (long long)(16 * mt + i) * ldc;
+#pragma unroll
+          for (int rg = 0; rg < T64_RG; ++rg) p[loo + 16 * rg] = Io<T>::from_f32(acc[rg][mt][i]);
+        }
+    }
+  } else {
+#pragma unroll
+    for (int rg = 0; rg < T64_RG; ++rg) {
+      const int row = r0 + 16 * rg + n;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = 16 * mt + 4 * g + i;
+          const bool go = (ABL & 32) ? acc[rg][mt][i] == 1.2345e30f : true;
+          if (go && t < M && row < N) {
+            if (ksplit > 1) ws[((long long)sp * M + t) * N + row] = acc[rg][mt][i];
+            else out[(long long)t * ldc + row] = Io<T>::from_f32(acc[rg][mt][i]);
+          }
+        }
+    }
+  }
+}
+
+// 0 = auto (33..64 tokens), 1 = off, 2 = forced wherever it applies (1..64 tokens; tests / A-B)
+int g_t64_mode = 0;
+int g_t64_ks = 0;                                            // lab: force the split count (0 = the rule)
+
+struct T64Geom {
+  int row_tiles, ksplit, kc;
+};
+static T64Geom t64_geometry(int m, int k) {
+  const int rt = (m + T64_ROWS - 1) / T64_ROWS, ngr = k / 256;
+  int cus = device_cu_count();
+  if (cus <= 0) cus = 256;
+  int ks = std::max(1, std::min(ngr, cus / std::max(1, rt)));   // one round of workgroups on the CUs
+  if (g_t64_ks > 0) ks = std::min(ngr, g_t64_ks);
+  const int kc = (ngr + ks - 1) / ks;
+  ks = (ngr + kc - 1) / kc;
+  return {rt, ks, kc};
+}
+
+bool t64_applicable(int m, int n, int k, int lda, int ldb, int blocksize, int blocksize2, bool nested, const void* A,
+                    const void* B) {
+  if (g_t64_mode == 1) return false;
+  if (n < 1 || n > 64 || ((g_t64_mode == 0 || g_t64_mode >= 16) && n < 33)) return false;
+  return m >= 1 && k >= 256 && k % 256 == 0 && blocksize == 64 && 2LL * ldb >= k && ldb % 128 == 0 &&
+         lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
+         (!nested || (blocksize2 >= 4 && (blocksize2 & (blocksize2 - 1)) == 0)) &&
+         (long long)(m - 1) * ldb + k / 2 < 0xFFFFFFFFLL && (long long)(n - 1) * lda * 2 + 2LL * k < 0x7FFFFFFFLL;
+}
+
+long long t64_workspace_bytes(int m, int n, int k) {
+  if (n < 1 || n > 64 || k < 256 || k % 256) return 0;
+  const T64Geom geo = t64_geometry(m, k);
+  return geo.ksplit > 1 ? (long long)geo.ksplit * n * m * (long long)sizeof(float) : 0;
+}
+
+// m = out features (weight rows), n = tokens, k = in features.  False: not applicable (nothing launched).
+template <typename T>
+bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
+                          int blocksize, int blocksize2, const float* code, T* out, int ldc, float* ws,
+                          long long ws_bytes) {
+  const bool nested = st.q8 != nullptr;
+  if (!t64_applicable(m, n, k, lda, ldb, blocksize, blocksize2, nested, A, B)) return false;
+  const T64Geom geo = t64_geometry(m, k);
+  if (geo.ksplit > 1 &&
+      (ws == nullptr || ((uintptr_t)ws & 15) || (long long)geo.ksplit * n * m * (long long)sizeof(float) > ws_bytes))
+    return false;
+  st.bs_shift = 6;
+  st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
+  const dim3 grid((unsigned)(geo.row_tiles * geo.ksplit));
+  auto lab = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc, ws,
+                       geo.ksplit, geo.kc);
+  };
+  if (g_t64_mode >= 16 && nested) {                          // lab ablations (nested bf16 / fp16 only)
+    switch (g_t64_mode - 16) {
+      case 1: lab(k_gemm_4bit_t64<T, true, 1>); break;
+      case 2: lab(k_gemm_4bit_t64<T, true, 2>); break;
+      case 4: lab(k_gemm_4bit_t64<T, true, 4>); break;
+      case 6: lab(k_gemm_4bit_t64<T, true, 6>); break;
+      case 8: lab(k_gemm_4bit_t64<T, true, 8>); break;
+      case 16: lab(k_gemm_4bit_t64<T, true, 16>); break;
+      case 24: lab(k_gemm_4bit_t64<T, true, 24>); break;
+      case 30: lab(k_gemm_4bit_t64<T, true, 30>); break;
+      case 32: lab(k_gemm_4bit_t64<T, true, 32>); break;
+      case 15: lab(k_gemm_4bit_t64<T, true>); break;
+      case 64: lab(k_gemm_4bit_t64<T, true, 64>); break;
+      case 128: lab(k_gemm_4bit_t64<T, true, 128>); break;
+      case 256: lab(k_gemm_4bit_t64<T, true, 256>); break;
+      case 30 + 32 + 64 + 128 + 256: lab(k_gemm_4bit_t64<T, true, 30 + 32 + 64 + 128 + 256>); break;
+      default: lab(k_gemm_4bit_t64<T, true>); break;
+    }
+  } else if (nested)
+    hipLaunchKernelGGL((k_gemm_4bit_t64<T, true>), grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb,
+                       st, code, out, ldc, ws, geo.ksplit, geo.kc);
+  else
+    hipLaunchKernelGGL((k_gemm_4bit_t64<T, false>), grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B,
+                       ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc);
+  if (geo.ksplit > 1 && g_t64_mode != 15) launch_splitk_rows_reduce<T>(ws, geo.ksplit, n, m, out, ldc);
+  return true;
+}
+
+template bool launch_gemm_4bit_t64<bf16_t>(int, int, int, const bf16_t*, int, const uint8_t*, int, SkStats, int, int,
+                                           const float*, bf16_t*, int, float*, long long);
+template bool launch_gemm_4bit_t64<fp16_t>(int, int, int, const fp16_t*, int, const uint8_t*, int, SkStats, int, int,
+                                           const float*, fp16_t*, int, float*, long long);
+
+}  // namespace bnb
+
+extern "C" {
+// [additive, testing] the 33..64-token kernel (gemm4bit_t64.hip): 0 = auto, 1 = off, 2 = wherever it applies (1..64
+// tokens); returns the previous setting
+int cgemm_4bit_set_t64_splits(int ks) {                   // [lab] force the split count (0 = the rule)
+  const int prev = bnb::g_t64_ks;
+  bnb::g_t64_ks = ks;
+  return prev;
+}
+int cgemm_4bit_set_t64_mode(int mode) {
+  BNB_RANGE("cgemm_4bit_set_t64_mode");
+  const int prev = bnb::g_t64_mode;
+  bnb::g_t64_mode = mode;
+  return prev;
+}
+}

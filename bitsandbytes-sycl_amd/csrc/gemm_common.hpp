@@ -93,6 +93,14 @@ struct SkStats {
   int bs_shift, bs2_shift;
 };
 long long skinny_workspace_bytes(int m, int n, int k);
+// the 33..64-token kernel (gemm4bit_t64.hip): fp32 split partials it needs (0: unsplit), and its launch (false: not
+// applicable, nothing launched)
+long long t64_workspace_bytes(int m, int n, int k);
+template <typename T>
+bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_t* B, int ldb, SkStats st,
+                          int blocksize, int blocksize2, const float* code, T* out, int ldc, float* ws,
+                          long long ws_bytes);
+int device_cu_count();
 // out[t, n] = T(sum_s ws[s][t][n]) (fp32 split partials, row-major [rows][cols] per split), splits summed in order
 template <typename T>
 void launch_splitk_rows_reduce(const float* ws, int nsplit, int rows, int cols, T* out, int ldc);

@@ -246,6 +246,9 @@ int chgemm_tn_pf_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb
                       const unsigned char* next_q8, const float* next_code2, const float* next_absmax2,
                       const float* next_offset, int fp4, int blocksize, int blocksize2, long long next_n,
                       bnb_fp16* next_out);
+/* [additive, testing] the 33..64-token 4-bit GEMM kernel (gemm4bit_t64.hip): 0 = auto (33..64 activation rows,
+ * blocksize 64, K % 256 == 0), 1 = off, 2 = wherever it applies (1..64 rows); returns the previous setting */
+int cgemm_4bit_set_t64_mode(int mode);
 /* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
  * grid_cap = at most that many workgroups (0 = none); returns the previous p */
 int cdequantize_set_stream_cfg(int p, int grid_cap);

@@ -1,0 +1,82 @@
+"""The 33..64-token kernel (gemm4bit_t64.hip): 192 weight rows x 64 tokens per workgroup, split-K with the ordered
+reduce, every operand by LDS-DMA.  Its arithmetic is the whole-K few-token kernel's (T(code) x tokens summed per
+64-element block on the MFMA, then x absmax), so the bar is the GEMV's / the tile kernels' against the fp64 oracle;
+deterministic; the in-kernel nested decode equals passing the decoded absmax.  Auto at 33..64 rows; forced
+(cgemm_4bit_set_t64_mode(2)) also at 1..32 rows; shapes it does not take (blocksize != 64, K % 256) fall back."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _F():
+    import python_src_quants.functional as F
+    return F
+
+
+def _close(got, exp, rtol, atol_rel):
+    rms = float(np.sqrt(np.mean(exp.astype(np.float64) ** 2))) + 1e-12
+    bad = np.abs(got - exp) > atol_rel * rms + rtol * np.abs(exp)
+    return float(bad.mean()), float(np.max(np.abs(got - exp)))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nested", [False, True])
+@pytest.mark.parametrize("qt,bs", [("nf4", 64), ("fp4", 64), ("nf4", 256)])
+@pytest.mark.parametrize("mnk,mode", [((33, 11008, 4096), 0), ((64, 11008, 4096), 0), ((48, 4096, 11008), 0),
+                                      ((64, 4096, 4096), 0), ((40, 1000, 2304), 0), ((64, 193, 256), 0),
+                                      ((57, 3584, 8192), 0), ((1, 4096, 4096), 2), ((17, 520, 768), 2)])
+def test_t64_vs_oracle(dev, dtype, nested, qt, bs, mnk, mode):
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(M * 7 + N + K + bs)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
+    prev = F.lib.cgemm_4bit_set_t64_mode(ct.c_int(mode))
+    saved = F.GEMM_4BIT_GEMV_TOKENS
+    F.GEMM_4BIT_GEMV_TOKENS = 1
+    F.set_fewtok_mode(1)                               # (forced rows <= 32: not the whole-K kernel)
+    try:
+        Y = F.gemm_4bit(X, q, st)
+        Y2 = F.gemm_4bit(X, q, st)
+        Yp = F.gemm_4bit(X, q, st, absmax=F._absmax_fp32(st))
+    finally:
+        F.lib.cgemm_4bit_set_t64_mode(ct.c_int(prev))
+        F.set_fewtok_mode(0)
+        F.GEMM_4BIT_GEMV_TOKENS = saved
+    assert Y.shape == (M, N) and Y.dtype == dtype
+    assert torch.equal(Y, Y2)                          # deterministic (splits summed in order)
+    assert torch.equal(Y, Yp)                          # in-kernel nested decode = the decoded absmax passed in
+    absmax = F._absmax_fp32(st).cpu().numpy()
+    exp = ref.gemm_4bit_dequant_ref(X.float().cpu().numpy(), q.cpu().numpy(), absmax, N, K, bs,
+                                    st.code.cpu().numpy(), "bf16" if dtype == torch.bfloat16 else "fp16")
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-2
+    frac, err = _close(Y.float().cpu().numpy(), exp, tol, tol)
+    assert frac == 0.0, err
+
+
+def test_t64_is_the_default_at_33_to_64_rows(dev):
+    """At 33..64 rows with blocksize 64 and K % 256 == 0 the auto rule takes the new kernel, and its result differs
+    from the split-K weight-stream kernel it replaced only within the tolerance (different block-sum association)."""
+    F = _F()
+    N, K, M = 11008, 4096, 64
+    torch.manual_seed(3)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    Y = F.gemm_4bit(X, q, st)
+    prev = F.lib.cgemm_4bit_set_t64_mode(ct.c_int(1))
+    try:
+        Yo = F.gemm_4bit(X, q, st)
+    finally:
+        F.lib.cgemm_4bit_set_t64_mode(ct.c_int(prev))
+    assert not torch.equal(Y, Yo)                      # a different kernel ran
+    e = Yo.float()
+    rms = e.pow(2).mean().sqrt()
+    assert bool(((Y.float() - e).abs() <= 2e-2 * rms + 2e-2 * e.abs()).all())

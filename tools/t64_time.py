@@ -1,0 +1,32 @@
+"""Time the few-token GEMM on the config-2 weight (11008 x 4096 NF4 nested, bf16) at 33..64 rows: the new kernel
+(gemm4bit_t64.hip) vs the split-K weight-stream kernel it replaces (cgemm_4bit_set_t64_mode(1)), HIP-graph replay over
+14 rotating weight copies (past the MALL), like bench.py's few-token leg."""
+import ctypes as ct
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "bitsandbytes-sycl_amd")]
+import python_src_quants.functional as F  # noqa: E402
+import bench  # noqa: E402
+
+dev = torch.device("cuda", 0)
+shapes = [(11008, 4096), (4096, 11008), (4096, 4096)]
+for N, K in shapes:
+    g = torch.Generator(device=dev).manual_seed(1)
+    copies = []
+    for _ in range(14 if N * K > 20_000_000 else 30):
+        W = (torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        copies.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True))
+    for M in (33, 48, 64):
+        X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+        outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in copies]
+        res = {}
+        for mode in (0, 1):
+            F.lib.cgemm_4bit_set_t64_mode(ct.c_int(mode))
+            calls = [(lambda q=q, s=s, o=o: F.gemm_4bit(X, q, s, out=o)) for (q, s), o in zip(copies, outs)]
+            res[mode] = bench._time_graph(calls, 10) * 1e6
+        F.lib.cgemm_4bit_set_t64_mode(ct.c_int(0))
+        print(f"{N}x{K} rows {M}: t64 {res[0]:.2f} us   previous (skinny) {res[1]:.2f} us")
