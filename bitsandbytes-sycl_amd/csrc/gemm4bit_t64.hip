@@ -44,7 +44,9 @@ constexpr int T64_STAT = 1024;                               // one statistics s
 constexpr int T64_OFF_TOK = T64_TABLE;
 constexpr int T64_OFF_W = T64_OFF_TOK + 2 * T64_TOK;
 constexpr int T64_OFF_S = T64_OFF_W + T64_WAVES * 2 * T64_WGRP;
-constexpr int T64_LDS = T64_OFF_S + T64_WAVES * 2 * T64_STAT;   // 150 KiB
+constexpr int T64_OFF_C2 = T64_OFF_S + T64_WAVES * 2 * T64_STAT;   // nested code map (256 floats)
+constexpr int T64_OFF_OFS = T64_OFF_C2 + 1024;                   // the nested offset (64 copies)
+constexpr int T64_LDS = T64_OFF_OFS + 256;                       // 153 KiB
 constexpr int T64_WPIECES = 16 * T64_RG / 8;                 // 6 weight pieces per wave per group
 constexpr int T64_TPIECES = 4;                               // token pieces per wave per half-group
 
@@ -91,36 +93,13 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   constexpr int TOPS = T64_TPIECES;                          // ... of one token half-group issue
   __shared__ __attribute__((aligned(16))) uint8_t sm[T64_LDS];
   uint8_t* table = sm;
-  auto code2s_at = [&](uint32_t t) -> const float& {
-    return *reinterpret_cast<const float*>(table + 256 * (t >> 5) + 128 + 4 * (t & 31));
-  };
+  auto code2s_at = [&](uint32_t t) -> const float& { return *reinterpret_cast<const float*>(sm + T64_OFF_C2 + 4 * t); };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 15, g = lane >> 4;
   const int bid = blockIdx.x, rt = bid / ksplit, sp = bid - rt * ksplit;
   const int r0 = rt * T64_ROWS + wave * 16 * T64_RG;         // this wave's first weight row
   const int ngr = K >> 8, gr0 = sp * kc, ng = min(kc, ngr - gr0);   // this workgroup's groups (>= 1, host rule)
-
-  // ---- the pair table (and the nested code map) before any DMA is in flight: hipcc's waits for these loads then wait
-  // for these loads alone.  Code values by scalar loads, selected per entry.
-  if constexpr ((ABL & 64) == 0) {
-    float dt[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) dt[j] = code[j];
-    float hi = dt[0], lo = dt[0];
-#pragma unroll
-    for (int j = 1; j < 16; ++j) {
-      hi = (tid >> 4) == j ? dt[j] : hi;
-      lo = (tid & 15) == j ? dt[j] : lo;
-    }
-    const uint32_t v = Dot2<T>::pair(hi, lo);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * tid + 16 * ((k + tid) & 7)) = make_uint4(v, v, v, v);
-    if constexpr (NESTED) *reinterpret_cast<float*>(table + 256 * (tid >> 5) + 128 + 4 * (tid & 31)) = st.code2[tid];
-  }
-  float offset = 0.0f;
-  if constexpr (NESTED) offset = *st.offset;
-  __builtin_amdgcn_s_waitcnt(0);                             // (table values in place before the stream starts)
 
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)sm);
   // token pieces: this wave's pieces q = 4 wave + i of a half-group slot; lane l -> token row t = 4 q + (l >> 4),
@@ -215,6 +194,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
           else xf[b2][mt][s] = *reinterpret_cast<const uint4*>(tk + (16 * mt + n) * 256 + 16 * (ls ^ n));
         }
     if constexpr (NESTED) {
+      const float offset = *reinterpret_cast<const float*>(sm + T64_OFF_OFS + 4 * (lane & 63));
 #pragma unroll
       for (int rg = 0; rg < T64_RG; ++rg)
 #pragma unroll
@@ -260,12 +240,36 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
       }
   };
 
-  // ---- prologue: W(0), T(0), T(1), W(1) -- the steady state's order (at each wait the ops younger than the awaited
-  // token half-group are exactly the next half-group's tokens and one weight group)
+  // ---- prologue: [code map], W(0), T(0), T(1), W(1) -- the steady state's order (at each wait the ops younger than
+  // the awaited token half-group are exactly the next half-group's tokens and one weight group; the code map is older)
+  if constexpr (NESTED) {
+    // (the offset too: a plain load of it would be a VMEM load hipcc waits for with vmcnt(0) -- inside the loop, where
+    // it drained every in-flight piece each group)
+    t64_dma<4>(st.code2, 4u * (uint32_t)(64 * wave + lane), lds0 + T64_OFF_C2 + 256 * wave);
+    if (wave == 0) t64_dma<4>(st.offset, 0u, lds0 + T64_OFF_OFS);
+  }
   issue_w(0, 0);
   issue_t(0, 0);
   issue_t(1, 1);
   issue_w(1, 1);
+  // ---- the pair table, built while the prologue's DMA is in flight (code values by scalar loads: lgkmcnt, not the
+  // vmcnt the DMA counts; the nested code map travels by LDS-DMA with the first pieces)
+  if constexpr ((ABL & 64) == 0) {
+    float dt[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dt[j] = code[j];
+    float hi = dt[0], lo = dt[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      hi = (tid >> 4) == j ? dt[j] : hi;
+      lo = (tid & 15) == j ? dt[j] : lo;
+    }
+    const uint32_t v = Dot2<T>::pair(hi, lo);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * tid + 16 * ((k + tid) & 7)) = make_uint4(v, v, v, v);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);                      // lgkmcnt(0): the table is written (barrier at the wait)
+
   for (int gi = 0; gi < ng; ++gi) {
     if constexpr ((ABL & 1) == 0)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(TOPS + WOPS) : "memory");   // T(2 gi) and W(gi) landed (this wave)
