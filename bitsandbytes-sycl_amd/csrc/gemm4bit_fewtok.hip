@@ -270,8 +270,34 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[rg][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto consume = [&](const Group& R, int gi, int slot) {
+  auto consume = [&](Group& R, int gi, int slot) {
     const uint8_t* gs = my_ring + slot * GB;
+    // pin this group's register loads here, behind wait_group: otherwise hipcc hoists their first uses (the statistics
+    // ds_bpermute) into the previous group's consume, and its wait for them -- the newest loads it can see -- is
+    // vmcnt(0), which also drains the DMA pieces issued after them (one group in flight instead of two)
+    if constexpr ((ABL & 1) == 0) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            if (!X8 || (bb & 1) == 0)
+              asm volatile("" : "+v"(R.x[bb][mt][s].x), "+v"(R.x[bb][mt][s].y), "+v"(R.x[bb][mt][s].z), "+v"(R.x[bb][mt][s].w));
+    }
+    if constexpr ((ABL & 2) == 0 && S4) {
+      if constexpr (NESTED) asm volatile("" : "+v"(R.q4), "+v"(R.a2g));
+      else asm volatile("" : "+v"(R.am4.x), "+v"(R.am4.y), "+v"(R.am4.z), "+v"(R.am4.w));
+    }
+    if constexpr ((ABL & 2) == 0 && !S4) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) {
+          if constexpr (NESTED) asm volatile("" : "+v"(R.q8[bb][rg]), "+v"(R.a2[bb][rg]));
+          else asm volatile("" : "+v"(R.am[bb][rg]));
+        }
+    }
     // S4: row group rg's statistics come from lane 16 rg + n (ds_bpermute, one per dword)
     uint32_t q4[S4 ? RG : 1];
     float a2g[S4 ? RG : 1];

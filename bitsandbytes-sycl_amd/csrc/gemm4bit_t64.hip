@@ -49,6 +49,9 @@ constexpr int T64_OFF_OFS = T64_OFF_C2 + 1024;                   // the nested o
 constexpr int T64_LDS = T64_OFF_OFS + 256;                       // 153 KiB
 constexpr int T64_WPIECES = 16 * T64_RG / 8;                 // 6 weight pieces per wave per group
 constexpr int T64_TPIECES = 4;                               // token pieces per wave per half-group
+constexpr int T64_STAGE_LD = T64_ROWS + 4;                  // staged partial tile row pitch (floats)
+static_assert(64 * T64_STAGE_LD * 4 <= T64_TABLE, "staged tile fits the table");
+typedef uint32_t hg_u32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T> struct T64Mfma;
 template <> struct T64Mfma<bf16_t> {
@@ -78,9 +81,93 @@ __device__ __forceinline__ void t64_dma_nt(const void* sbase, uint32_t voff, uin
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" : : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
 
+typedef float t64_f32x2_t __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ uint32_t t64_cvt2(float a, float b) {   // one RNE cast each
+  if constexpr (std::is_same<T, bf16_t>::value)
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((t64_f32x2_t){a, b}, bf16x2_t));
+  else
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((t64_f32x2_t){a, b}, f16x2_t));
+}
+
+// device-scope (sc1) dword store / loads of the fp32 partials through a buffer resource (element offsets < 2^29)
+__device__ __forceinline__ void t64_store_dev(__amdgpu_buffer_rsrc_t r, uint32_t e, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)(4u * e), 0, 16);
+}
+__device__ __forceinline__ float4 t64_load4_dev(__amdgpu_buffer_rsrc_t r, uint32_t e) {
+  // (the whole vector cast: hipcc's bit_cast of one subscripted element of this builtin's result reads element 0)
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(4u * e), 0, 16));
+}
+__device__ __forceinline__ float t64_load_dev(__amdgpu_buffer_rsrc_t r, uint32_t e) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(4u * e), 0, 16));
+}
+
+// The split-K combine of one row tile (rows row0 .. row0 + 191, every token), run by the row tile's last workgroup to
+// finish: out[t][row] = T(ws[0][t][row] + ws[1][t][row] + ... ) -- k_skinny_reduce's additions in its order, so the
+// outputs are bit-identical to the two-launch form.
+template <typename T>
+__device__ __forceinline__ void t64_combine(__amdgpu_buffer_rsrc_t wsr, int ks, int M, int N, int row0,
+                                            T* __restrict__ out, int ldc, int tid) {
+  const uint32_t mn = (uint32_t)M * (uint32_t)N;
+  const int rows = min(T64_ROWS, N - row0);
+  if ((N & 3) == 0) {                                        // row0 % 4 == 0 too: whole float4s
+    // element e = tid + 256 j (j < 12 covers 64 tokens x 48 float4s): every load of KB splits x 12 elements in
+    // flight before the adds -- one round trip per KB splits instead of one per element
+    constexpr int EPT = (64 * T64_ROWS / 4) / T64_THREADS, KB = 4;
+    const int per_t = rows >> 2, total = M * per_t;
+    const bool st8 = (((uintptr_t)out & 7) == 0) && (ldc & 3) == 0;
+    uint32_t off[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = min(tid + T64_THREADS * j, total - 1), t = e / per_t, c = e - t * per_t;
+      off[j] = (uint32_t)t * (uint32_t)N + (uint32_t)(row0 + 4 * c);
+    }
+    float4 s[EPT];
+    for (int k0 = 0; k0 < ks; k0 += KB) {
+      float4 v[KB][EPT];
+#pragma unroll
+      for (int b = 0; b < KB; ++b)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j)
+          if (k0 + b < ks) v[b][j] = t64_load4_dev(wsr, (uint32_t)(k0 + b) * mn + off[j]);
+#pragma unroll
+      for (int b = 0; b < KB; ++b)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+          if (k0 + b == 0) {
+            s[j] = v[0][j];
+          } else if (k0 + b < ks) {
+            s[j].x += v[b][j].x; s[j].y += v[b][j].y; s[j].z += v[b][j].z; s[j].w += v[b][j].w;
+          }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = tid + T64_THREADS * j;
+      if (e >= total) break;
+      const int t = e / per_t, c = e - t * per_t;
+      T* dst = out + (long long)t * ldc + row0 + 4 * c;
+      if (st8) {
+        *reinterpret_cast<uint2*>(dst) = make_uint2(t64_cvt2<T>(s[j].x, s[j].y), t64_cvt2<T>(s[j].z, s[j].w));
+      } else {
+        dst[0] = Io<T>::from_f32(s[j].x); dst[1] = Io<T>::from_f32(s[j].y);
+        dst[2] = Io<T>::from_f32(s[j].z); dst[3] = Io<T>::from_f32(s[j].w);
+      }
+    }
+  } else {
+    for (int e = tid; e < M * rows; e += T64_THREADS) {
+      const int t = e / rows, r = e - t * rows;
+      const uint32_t off = (uint32_t)t * (uint32_t)N + (uint32_t)(row0 + r);
+      float s = t64_load_dev(wsr, off);
+      for (int k = 1; k < ks; ++k) s += t64_load_dev(wsr, (uint32_t)k * mn + off);
+      out[(long long)t * ldc + row0 + r] = Io<T>::from_f32(s);
+    }
+  }
+}
+
 // N = out features (weight rows), M = tokens (1..64), K = in features (% 256 == 0), blocksize 64.  Workgroup
 // (row tile rt, split sp): rows rt * 192 .., groups [sp * kc, min((sp + 1) * kc, K / 256)).  ksplit > 1: fp32
-// partials ws[sp][token][row]; else the outputs.
+// partials ws[sp][token][row], combined by the row tile's last workgroup when `tickets` is given (one counter per row
+// tile, zero between launches), else by k_skinny_reduce after the launch; ksplit == 1: the outputs.
 // ABL (lab ablations, timing only): 1 = no vmcnt waits, 2 = no token DMA after the prologue, 4 = no weight DMA after
 // the prologue, 8 = no MFMAs, 16 = no table lookups, 32 = no output / partial stores, 64 = no table build, 128 = no
 // barriers in the loop, 256 = no token fragment reads
@@ -88,7 +175,7 @@ template <typename T, bool NESTED, int ABL = 0>
 __global__ void __launch_bounds__(T64_THREADS, 1)
 k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
                 SkStats st, const float* __restrict__ code, T* __restrict__ out, int ldc, float* __restrict__ ws,
-                int ksplit, int kc) {
+                int ksplit, int kc, uint32_t* __restrict__ tickets) {
   constexpr int WOPS = (NESTED ? 2 : 1) + T64_WPIECES;       // VMEM instructions of one weight-group issue
   constexpr int TOPS = T64_TPIECES;                          // ... of one token half-group issue
   __shared__ __attribute__((aligned(16))) uint8_t sm[T64_LDS];
@@ -298,9 +385,39 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   // range) stores unpredicated from a wave-uniform base per (token tile, i) plus one 32-bit lane offset; edge tiles
   // check every element.
   const bool whole = M == 64 && rt * T64_ROWS + T64_ROWS <= N;
+  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7FFFFFFF, 0x00020000);
   if (whole && (ABL & 32) == 0) {
     const uint32_t loff = (uint32_t)(4 * g) * (uint32_t)N + (uint32_t)(r0 + n);
-    if (ksplit > 1) {
+    if (ksplit > 1 && tickets != nullptr && (N & 3) == 0) {
+      // device-scope stores (the combine reads them), whole lines: the tile through LDS ([token][row], rows padded to
+      // 196 floats: the 4 token rows of one write are 2-way on the banks) then 16-B stores, each wave's 1 KiB contiguous
+      float* stage = reinterpret_cast<float*>(sm);             // the table: every wave is past its last lookup
+      __syncthreads();
+      const int wr0 = wave * 16 * T64_RG;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int rg = 0; rg < T64_RG; ++rg) stage[(16 * mt + 4 * g + i) * T64_STAGE_LD + wr0 + 16 * rg + n] = acc[rg][mt][i];
+      __syncthreads();
+      const uint32_t b0 = (uint32_t)sp * 64u * (uint32_t)N + (uint32_t)(rt * T64_ROWS);
+#pragma unroll
+      for (int j = 0; j < (64 * T64_ROWS / 4) / T64_THREADS; ++j) {
+        const int e = tid + T64_THREADS * j, t = e / (T64_ROWS / 4), c = e - t * (T64_ROWS / 4);
+        const float4 v = *reinterpret_cast<const float4*>(stage + t * T64_STAGE_LD + 4 * c);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hg_u32x4, v), wsr, (int)(4u * (b0 + (uint32_t)t * (uint32_t)N + 4u * c)), 0, 16);
+      }
+    } else if (ksplit > 1 && tickets != nullptr) {
+      const uint32_t b0 = (uint32_t)sp * 64u * (uint32_t)N + loff;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int rg = 0; rg < T64_RG; ++rg)
+            t64_store_dev(wsr, b0 + (uint32_t)(16 * mt + i) * (uint32_t)N + 16u * rg, acc[rg][mt][i]);
+    } else if (ksplit > 1) {
       float* wsb = ws + (long long)sp * 64 * N;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -332,17 +449,62 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
           const int t = 16 * mt + 4 * g + i;
           const bool go = (ABL & 32) ? acc[rg][mt][i] == 1.2345e30f : true;
           if (go && t < M && row < N) {
-            if (ksplit > 1) ws[((long long)sp * M + t) * N + row] = acc[rg][mt][i];
+            if (ksplit > 1 && tickets != nullptr) t64_store_dev(wsr, ((uint32_t)sp * (uint32_t)M + t) * (uint32_t)N + row, acc[rg][mt][i]);
+            else if (ksplit > 1) ws[((long long)sp * M + t) * N + row] = acc[rg][mt][i];
             else out[(long long)t * ldc + row] = Io<T>::from_f32(acc[rg][mt][i]);
           }
         }
     }
   }
+
+  // ---- split-K combine by the row tile's last workgroup to finish.  Hand-off (the condition the round-2
+  // combine missed): the partials are device-scope stores (sc1: coherent across the XCDs' L2s without a cache-wide
+  // write-back), every wave waits for its own to complete (vmcnt(0)), a barrier, then one device-scope ticket per
+  // workgroup; the last arriver reads the partials with device-scope loads.  No workgroup waits for another (nothing
+  // spins), and no L2 write-back / invalidate runs (those, as agent fences, cost 35-55 us here: every wave's write-back
+  // plus the invalidate evicting the tokens of the workgroups still running).  The last arriver resets the ticket.
+  if (tickets != nullptr && ksplit > 1 && (ABL & 32) == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile uint32_t* last = reinterpret_cast<volatile uint32_t*>(sm);   // the table: no DMA is in flight any more
+    if (tid == 0)
+      last[0] = __hip_atomic_fetch_add(&tickets[rt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                (uint32_t)(ksplit - 1) ? 1u : 0u;
+    __syncthreads();
+    if (last[0] == 0u) return;
+    t64_combine<T>(wsr, ksplit, M, N, rt * T64_ROWS, out, ldc, tid);
+    if (tid == 0) __hip_atomic_store(&tickets[rt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
+
+// One ticket per row tile, in T64_TICKET_SETS sets handed out round-robin to launches, so launches in flight on
+// different streams at the same time do not share counters (every counter is back at zero when its launch ends).
+constexpr int T64_MAX_TILES = 1024, T64_TICKET_SETS = 16;
+__device__ uint32_t g_t64_tickets[T64_TICKET_SETS * T64_MAX_TILES];
 
 // 0 = auto (33..64 tokens), 1 = off, 2 = forced wherever it applies (1..64 tokens; tests / A-B)
 int g_t64_mode = 0;
 int g_t64_ks = 0;                                            // lab: force the split count (0 = the rule)
+// 1: in-kernel last-arriver combine, 0 (default): k_skinny_reduce.  Measured (tools/t64_time.py,
+// profiles/lab/r04_t64.txt): 11008 x 4096 at 64 rows 25.7 us in-kernel vs 22.6 us with the reduce launch -- the combine
+// of a row tile is one workgroup reading 192 KiB of device-scope partials (8.6 us of tail on 58 CUs), the reduce
+// launch spreads the same reads over ~700 workgroups for 5.7 us
+int g_t64_combine = 0;
+
+// this launch's ticket set on the current device (nullptr: use the reduce launch)
+static uint32_t* t64_tickets(int row_tiles, long long partial_bytes) {
+  if (!g_t64_combine || row_tiles > T64_MAX_TILES || partial_bytes > 0x7FFFFFFFLL) return nullptr;
+  static uint32_t* base[64] = {};
+  static unsigned next[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (base[dev] == nullptr) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_t64_tickets)) != hipSuccess) return nullptr;
+    base[dev] = static_cast<uint32_t*>(p);
+  }
+  return base[dev] + (next[dev]++ % T64_TICKET_SETS) * T64_MAX_TILES;
+}
 
 struct T64Geom {
   int row_tiles, ksplit, kc;
@@ -388,9 +550,10 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
   st.bs_shift = 6;
   st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
   const dim3 grid((unsigned)(geo.row_tiles * geo.ksplit));
+  uint32_t* tickets = geo.ksplit > 1 && g_t64_mode != 15 ? t64_tickets(geo.row_tiles, (long long)geo.ksplit * n * m * 4) : nullptr;
   auto lab = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc, ws,
-                       geo.ksplit, geo.kc);
+                       geo.ksplit, geo.kc, tickets);
   };
   if (g_t64_mode >= 16 && nested) {                          // lab ablations (nested bf16 / fp16 only)
     switch (g_t64_mode - 16) {
@@ -412,11 +575,12 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
     }
   } else if (nested)
     hipLaunchKernelGGL((k_gemm_4bit_t64<T, true>), grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb,
-                       st, code, out, ldc, ws, geo.ksplit, geo.kc);
+                       st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets);
   else
     hipLaunchKernelGGL((k_gemm_4bit_t64<T, false>), grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B,
-                       ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc);
-  if (geo.ksplit > 1 && g_t64_mode != 15) launch_splitk_rows_reduce<T>(ws, geo.ksplit, n, m, out, ldc);
+                       ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets);
+  if (geo.ksplit > 1 && g_t64_mode != 15 && tickets == nullptr)
+    launch_splitk_rows_reduce<T>(ws, geo.ksplit, n, m, out, ldc);
   return true;
 }
 
@@ -433,6 +597,13 @@ extern "C" {
 int cgemm_4bit_set_t64_splits(int ks) {                   // [lab] force the split count (0 = the rule)
   const int prev = bnb::g_t64_ks;
   bnb::g_t64_ks = ks;
+  return prev;
+}
+// [additive, testing] split-K combine of the 33..64-token kernel: 1 = in the kernel (last workgroup of each row tile),
+// 0 (default) = the separate reduce launch; returns the previous setting
+int cgemm_4bit_set_t64_combine(int on) {
+  const int prev = bnb::g_t64_combine;
+  bnb::g_t64_combine = on ? 1 : 0;
   return prev;
 }
 int cgemm_4bit_set_t64_mode(int mode) {

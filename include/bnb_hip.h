@@ -249,6 +249,10 @@ int chgemm_tn_pf_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb
 /* [additive, testing] the 33..64-token 4-bit GEMM kernel (gemm4bit_t64.hip): 0 = auto (33..64 activation rows,
  * blocksize 64, K % 256 == 0), 1 = off, 2 = wherever it applies (1..64 rows); returns the previous setting */
 int cgemm_4bit_set_t64_mode(int mode);
+/* [additive, testing] split-K combine of that kernel: 1 = by the last workgroup of each row tile to finish (device-scope
+ * partials, vmcnt(0) + barrier, then a ticket; splits summed in order), 0 (default) = a separate reduce launch (faster:
+ * DESIGN.md §4); returns the previous setting */
+int cgemm_4bit_set_t64_combine(int on);
 /* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
  * grid_cap = at most that many workgroups (0 = none); returns the previous p */
 int cdequantize_set_stream_cfg(int p, int grid_cap);

@@ -80,3 +80,50 @@ def test_t64_is_the_default_at_33_to_64_rows(dev):
     e = Yo.float()
     rms = e.pow(2).mean().sqrt()
     assert bool(((Y.float() - e).abs() <= 2e-2 * rms + 2e-2 * e.abs()).all())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mnk", [(64, 11008, 4096), (33, 4096, 11008), (40, 1000, 2304), (64, 193, 4096),
+                                 (57, 3584, 8192), (48, 520, 4096)])
+@pytest.mark.parametrize("splits", [0, 3, 11])
+def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
+    """The split-K partials summed by each row tile's last workgroup to finish (agent-scope release / acquire
+    hand-off, one ticket per row tile) equal the separate k_skinny_reduce launch bit for bit: same additions in split
+    order; whole float4 rows (N % 4 == 0, partial last row tile) and the scalar form (N = 193); more than 8 splits
+    (the batched loads' second round).  Ten launches in a row and a HIP-graph replay: every ticket is back at zero
+    after its launch."""
+    F = _F()
+    M, N, K = mnk
+    torch.manual_seed(N + K + M)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(dtype)
+    X = torch.randn(M, K, device=dev, dtype=dtype)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    prev_ks = F.lib.cgemm_4bit_set_t64_splits(ct.c_int(splits))
+    prev_mode = F.lib.cgemm_4bit_set_t64_mode(ct.c_int(2))
+    try:
+        F.lib.cgemm_4bit_set_t64_combine(ct.c_int(0))
+        ref_out = F.gemm_4bit(X, q, st)
+        F.lib.cgemm_4bit_set_t64_combine(ct.c_int(1))
+        outs = [F.gemm_4bit(X, q, st) for _ in range(10)]
+        out = torch.empty_like(ref_out)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            F.gemm_4bit(X, q, st, out=out)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                F.gemm_4bit(X, q, st, out=out)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        replays = []
+        for _ in range(3):
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            replays.append(out.clone())
+    finally:
+        F.lib.cgemm_4bit_set_t64_combine(ct.c_int(0))
+        F.lib.cgemm_4bit_set_t64_mode(ct.c_int(prev_mode))
+        F.lib.cgemm_4bit_set_t64_splits(ct.c_int(prev_ks))
+    for o in outs + replays:
+        assert torch.equal(o, ref_out)

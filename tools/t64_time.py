@@ -24,9 +24,14 @@ for N, K in shapes:
         X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
         outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in copies]
         res = {}
-        for mode in (0, 1):
-            F.lib.cgemm_4bit_set_t64_mode(ct.c_int(mode))
-            calls = [(lambda q=q, s=s, o=o: F.gemm_4bit(X, q, s, out=o)) for (q, s), o in zip(copies, outs)]
-            res[mode] = bench._time_graph(calls, 10) * 1e6
+        for rnd in range(3):                                  # interleaved rounds, median
+            for arm, (mode, comb) in {"t64": (0, 1), "t64_reduce_launch": (0, 0), "skinny": (1, 1)}.items():
+                F.lib.cgemm_4bit_set_t64_mode(ct.c_int(mode))
+                F.lib.cgemm_4bit_set_t64_combine(ct.c_int(comb))
+                calls = [(lambda q=q, s=s, o=o: F.gemm_4bit(X, q, s, out=o)) for (q, s), o in zip(copies, outs)]
+                res.setdefault(arm, []).append(bench._time_graph(calls, 10) * 1e6)
         F.lib.cgemm_4bit_set_t64_mode(ct.c_int(0))
-        print(f"{N}x{K} rows {M}: t64 {res[0]:.2f} us   previous (skinny) {res[1]:.2f} us")
+        F.lib.cgemm_4bit_set_t64_combine(ct.c_int(1))
+        med = {a: sorted(v)[1] for a, v in res.items()}
+        print(f"{N}x{K} rows {M}: t64 (in-kernel combine) {med['t64']:.2f} us   t64 + reduce launch "
+              f"{med['t64_reduce_launch']:.2f} us   previous (skinny) {med['skinny']:.2f} us", flush=True)
