@@ -372,7 +372,8 @@ def bench_few_token_gemm(dev, iters=30, tokens=(2, 4, 8, 16, 32, 64)):
         del W
     res = {"shape": [None, n_out, k_in],
            "path": "2..32 rows: k_gemm_4bit_fewtok (whole K per workgroup, LDS-DMA weight ring, 16x16x32 MFMA, one "
-                   "launch); 33..64 rows: k_gemm_4bit_skinny (+ k_skinny_reduce)"}
+                   "launch); 33..64 rows: k_gemm_4bit_t64 (192 weight rows x 64 tokens per workgroup, split-K, "
+                   "+ k_skinny_reduce)"}
     for m in tokens:
         x = torch.randn(m, k_in, device=dev, dtype=torch.bfloat16, generator=g)
         out = torch.empty(m, n_out, device=dev, dtype=torch.bfloat16)
@@ -956,8 +957,10 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (seeded randn; W ~ N(0,0.02) -> NF4 bs=64 nested stats; X ~ N(0,1) bf16)",
             "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (functional.gemm_4bit: HIP "
-                                   "dequantise + the hand-written bf16 GEMM k_hgemm at this M, the dequantise of each "
-                                   "step's weight run inside the previous step's k_hgemm (prefetch); fused dequant+MFMA "
+                                   "dequantise + the hand-written bf16 GEMM k_hgemm at this M"
+                                   + ("; the dequantise of each step's weight run inside the previous step's k_hgemm "
+                                      "(--prefetch)" if PREFETCH[0] else ", every step dequantising its weight") +
+                                   "; fused dequant+MFMA "
                                    f"kernel below {F.GEMM_4BIT_DEQUANT_MIN_ROWS} rows / "
                                    f"{F.GEMM_4BIT_DEQUANT_MIN_FEATURES} features) + bf16 all-gather of output-column "
                                    "shards",
