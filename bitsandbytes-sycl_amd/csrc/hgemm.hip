@@ -171,6 +171,12 @@ __device__ __forceinline__ uint32_t mm_dequant_pair(int32_t a0, int32_t a1, floa
 // 127.3-129.3 vs 128.7-129.3 us; tools/hgemm_variant_ab.py, profiles/lab/r04_hgemm_variants.txt).  The round-3
 // two-half schedule stays selectable at run time (chgemm_set_variant(1)) as the A/B arm.
 constexpr int HG_V = 16 + 8192;
+// variant bit: the full-tile 16-bit epilogue stores C write-through (sc1), so the launch ends with no dirty L2 lines for
+// the next kernel's boundary to write back (chgemm_set_c_store; on by default: int8 igemmlt+dequant at the metric shape
+// 126.3 -> 124.8 us, config 3 52.7 -> 51.7 us, the NF4 step unchanged to -1 us, C4 unchanged;
+// profiles/lab/r04_store_policy.txt)
+constexpr int HG_V_CWT = 32768;
+static int g_hg_cwt = 1;
 constexpr int HG_V_ALT = 8 + 16 + 4096;
 static int g_hgemm_variant = 0;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
@@ -845,7 +851,11 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     for (int it = 0; it < 16 * WI / RPI; ++it) {
       const int row = RPI * it + lane_e / CPR, c16 = lane_e % CPR;
       const uint4 v = *reinterpret_cast<const uint4*>(ep + row * EPI_PITCH + 16 * c16);
-      *reinterpret_cast<uint4*>(cbase + (long long)row * ldc * 2 + 16 * c16) = v;
+      uint8_t* dst = cbase + (long long)row * ldc * 2 + 16 * c16;
+      if constexpr ((V & HG_V_CWT) != 0)                 // device-scope write-through: C leaves no dirty L2 lines
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"((hg_u32x4_t){v.x, v.y, v.z, v.w}) : "memory");
+      else
+        *reinterpret_cast<uint4*>(dst) = v;
     }
   } else if (full) {
     if constexpr (OP == HG_I8_I32) {                   // int32: one 16-B store per accumulator already
@@ -1009,6 +1019,9 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
     pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, false, full_only);      // no (large enough) workspace: no split
   if (g_hgemm_variant == 1) {
     hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
+  } else if (pl.wi == 8 && pl.wj == 8 && pl.splits == 1 && g_hg_cwt) {
+    hgemm_launch_shape<OP, HG_V | HG_V_CWT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws,
+                                                  side);
   } else if (pl.wi == 8 && pl.wj == 8) {
     hgemm_launch_shape<OP, HG_V, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
   } else if constexpr (FP) {
@@ -1123,6 +1136,13 @@ void chgemm_tn_plan(int m, int n, int k, int* out) {
   out[3] = pl.kchunk;
 }
 // [additive, testing] the side dequantise's A/B bits (HgSide::mode); returns the previous setting
+// [additive, testing] 1 (default): the 256 x 256 k_hgemm stores C write-through (sc1), 0: write-back; returns the
+// previous setting
+int chgemm_set_c_store(int wt) {
+  const int prev = bnb::g_hg_cwt;
+  bnb::g_hg_cwt = wt ? 1 : 0;
+  return prev;
+}
 int chgemm_set_side_mode(int v) {
   BNB_RANGE("chgemm_set_side_mode");
   const int prev = bnb::g_side_mode;

@@ -258,7 +258,10 @@ struct NestedStats {
   int bs2_shift;
 };
 
-template <typename T, int DT, int P, bool NESTED = false>
+// STP: store policy of the 16-B output stores -- 0 default (write-back L2), 1 non-temporal (nt), 2 device-scope
+// write-through (sc1, through a buffer resource: the output below 2 GiB)
+typedef uint32_t dq_u32x4 __attribute__((ext_vector_type(4)));
+template <typename T, int DT, int P, bool NESTED = false, int STP = 0>
 __global__ void __launch_bounds__(256)
 k_dequantize_4bit_stream(const uint8_t* __restrict__ A, const float* __restrict__ absmax, T* __restrict__ out,
                          int bs_shift, long long ndw, NestedStats ns = {}) {
@@ -301,7 +304,14 @@ k_dequantize_4bit_stream(const uint8_t* __restrict__ A, const float* __restrict_
         uint4 o;
         o.x = Pack2<T>::pk(v[0], v[1]); o.y = Pack2<T>::pk(v[2], v[3]);
         o.z = Pack2<T>::pk(v[4], v[5]); o.w = Pack2<T>::pk(v[6], v[7]);
-        reinterpret_cast<uint4*>(out)[d] = o;
+        if constexpr (STP == 1) {
+          __builtin_nontemporal_store((dq_u32x4){o.x, o.y, o.z, o.w}, reinterpret_cast<dq_u32x4*>(out) + d);
+        } else if constexpr (STP == 2) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7FFFFFFF, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128((dq_u32x4){o.x, o.y, o.z, o.w}, r, (int)(16 * d), 0, 16);
+        } else {
+          reinterpret_cast<uint4*>(out)[d] = o;
+        }
       }
     }
   }
@@ -397,7 +407,11 @@ void quantize_blockwise(const float* code, const T* A, float* absmax, uint8_t* o
 
 // Launch shape of k_dequantize_4bit_stream (A/B knob cdequantize_set_stream_cfg): dwords per lane per pass (4, 8 or 16)
 // and a cap on the grid (0: one pass per workgroup; else at most that many workgroups, grid-stride passes)
-static int g_dq_p = 8, g_dq_grid_cap = 0;
+// store policy (cdequantize_set_store_policy): 2 = write-through by default.  The 90 MB bf16 weight of the metric step
+// then leaves no dirty L2 lines for the kernel end / boundary to write back: the dequantise alone 23.1 -> 14.9 us, the
+// metric step 263.3 -> 260.2 us, C1 8.85 -> 8.6 us; non-temporal stores 20.8 us alone but a slower step (266.0)
+// (tools/dequant_store_ab.py, tools/bench_knobs.py; profiles/lab/r04_store_policy.txt)
+static int g_dq_p = 8, g_dq_grid_cap = 0, g_dq_store = 2;
 template <typename T, int DT, bool NESTED>
 static void launch_dq_stream(const uint8_t* A, const float* absmax, T* out, int bs_shift, long long ndw,
                              const NestedStats& ns) {
@@ -406,8 +420,14 @@ static void launch_dq_stream(const uint8_t* A, const float* absmax, T* out, int 
     long long wgs = (ndw + 256 * P - 1) / (256 * P);
     if (wgs > 65536) wgs = 65536;
     if (g_dq_grid_cap > 0 && wgs > g_dq_grid_cap) wgs = g_dq_grid_cap;
-    hipLaunchKernelGGL((k_dequantize_4bit_stream<T, DT, P, NESTED>), dim3((int)wgs), dim3(256), 0, current_stream(), A,
-                       absmax, out, bs_shift, ndw, ns);
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((int)wgs), dim3(256), 0, current_stream(), A, absmax, out, bs_shift, ndw, ns);
+    };
+    if constexpr (P == 8 && sizeof(T) == 2) {               // store-policy variants (the default shape only)
+      if (g_dq_store == 1) return launch(k_dequantize_4bit_stream<T, DT, P, NESTED, 1>);
+      if (g_dq_store == 2 && ndw * 16 <= 0x7FFFFFFFLL) return launch(k_dequantize_4bit_stream<T, DT, P, NESTED, 2>);
+    }
+    launch(k_dequantize_4bit_stream<T, DT, P, NESTED>);
   };
   if (g_dq_p == 4) go(std::integral_constant<int, 4>{});
   else if (g_dq_p == 16) go(std::integral_constant<int, 16>{});
@@ -492,6 +512,13 @@ int cdequantize_set_stream_cfg(int p, int grid_cap) {
   const int prev = g_dq_p;
   g_dq_p = p;
   g_dq_grid_cap = grid_cap;
+  return prev;
+}
+// [additive, testing] store policy of k_dequantize_4bit_stream's 16-bit outputs (default launch shape): 0 = write-back,
+// 1 = non-temporal, 2 (default) = device-scope write-through; returns the previous setting
+int cdequantize_set_store_policy(int policy) {
+  const int prev = g_dq_store;
+  g_dq_store = policy;
   return prev;
 }
 

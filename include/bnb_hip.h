@@ -256,8 +256,14 @@ int cgemm_4bit_set_t64_combine(int on);
 /* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
  * grid_cap = at most that many workgroups (0 = none); returns the previous p */
 int cdequantize_set_stream_cfg(int p, int grid_cap);
+/* [additive, testing] store policy of that kernel's bf16/fp16 outputs: 0 = write-back, 1 = non-temporal,
+ * 2 (default) = device-scope write-through; returns the previous setting */
+int cdequantize_set_store_policy(int policy);
 /* [additive, testing] k_hgemm side-dequantise A/B bits (chgemm_tn_pf_*); returns the previous value */
 int chgemm_set_side_mode(int v);
+/* [additive, testing] 1 (default): the 256 x 256 k_hgemm stores C write-through (device scope), 0: write-back;
+ * returns the previous setting */
+int chgemm_set_c_store(int wt);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);
 /* [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k): out = {WI, WJ, splits, k-tiles per split};
