@@ -175,7 +175,7 @@ template <typename T, bool NESTED, int ABL = 0>
 __global__ void __launch_bounds__(T64_THREADS, 1)
 k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
                 SkStats st, const float* __restrict__ code, T* __restrict__ out, int ldc, float* __restrict__ ws,
-                int ksplit, int kc, uint32_t* __restrict__ tickets) {
+                int ksplit, int kc, uint32_t* __restrict__ tickets, int pstore) {
   constexpr int WOPS = (NESTED ? 2 : 1) + T64_WPIECES;       // VMEM instructions of one weight-group issue
   constexpr int TOPS = T64_TPIECES;                          // ... of one token half-group issue
   __shared__ __attribute__((aligned(16))) uint8_t sm[T64_LDS];
@@ -386,9 +386,12 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   // check every element.
   const bool whole = M == 64 && rt * T64_ROWS + T64_ROWS <= N;
   const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7FFFFFFF, 0x00020000);
+  // partial stores: 0 plain, 1 device-scope (sc1) dwords, 2 device-scope 16-B lines staged through LDS (the combine
+  // needs device scope; for the reduce launch it only saves the boundary's write-back of dirty lines)
+  const int wt = tickets != nullptr ? 2 : pstore;
   if (whole && (ABL & 32) == 0) {
     const uint32_t loff = (uint32_t)(4 * g) * (uint32_t)N + (uint32_t)(r0 + n);
-    if (ksplit > 1 && tickets != nullptr && (N & 3) == 0) {
+    if (ksplit > 1 && wt == 2 && (N & 3) == 0) {
       // device-scope stores (the combine reads them), whole lines: the tile through LDS ([token][row], rows padded to
       // 196 floats: the 4 token rows of one write are 2-way on the banks) then 16-B stores, each wave's 1 KiB contiguous
       float* stage = reinterpret_cast<float*>(sm);             // the table: every wave is past its last lookup
@@ -408,7 +411,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
         const float4 v = *reinterpret_cast<const float4*>(stage + t * T64_STAGE_LD + 4 * c);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hg_u32x4, v), wsr, (int)(4u * (b0 + (uint32_t)t * (uint32_t)N + 4u * c)), 0, 16);
       }
-    } else if (ksplit > 1 && tickets != nullptr) {
+    } else if (ksplit > 1 && wt != 0) {
       const uint32_t b0 = (uint32_t)sp * 64u * (uint32_t)N + loff;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -449,7 +452,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
           const int t = 16 * mt + 4 * g + i;
           const bool go = (ABL & 32) ? acc[rg][mt][i] == 1.2345e30f : true;
           if (go && t < M && row < N) {
-            if (ksplit > 1 && tickets != nullptr) t64_store_dev(wsr, ((uint32_t)sp * (uint32_t)M + t) * (uint32_t)N + row, acc[rg][mt][i]);
+            if (ksplit > 1 && wt != 0) t64_store_dev(wsr, ((uint32_t)sp * (uint32_t)M + t) * (uint32_t)N + row, acc[rg][mt][i]);
             else if (ksplit > 1) ws[((long long)sp * M + t) * N + row] = acc[rg][mt][i];
             else out[(long long)t * ldc + row] = Io<T>::from_f32(acc[rg][mt][i]);
           }
@@ -490,6 +493,10 @@ int g_t64_ks = 0;                                            // lab: force the s
 // of a row tile is one workgroup reading 192 KiB of device-scope partials (8.6 us of tail on 58 CUs), the reduce
 // launch spreads the same reads over ~700 workgroups for 5.7 us
 int g_t64_combine = 0;
+// partial-store policy (cgemm_4bit_set_t64_pstore): 2 = write-through 16-B lines by default -- the reduce launch's
+// boundary then has no dirty partials to write back (11008 x 4096 at 64 rows 22.9 -> 21.8 us, 4096 x 11008 24.7 ->
+// 22.3, 4096^2 19.0 -> 15.5; write-through dwords within 0.2 us of the lines; profiles/lab/r04_t64.txt)
+int g_t64_pstore = 2;
 
 // this launch's ticket set on the current device (nullptr: use the reduce launch)
 static uint32_t* t64_tickets(int row_tiles, long long partial_bytes) {
@@ -551,9 +558,10 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
   st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
   const dim3 grid((unsigned)(geo.row_tiles * geo.ksplit));
   uint32_t* tickets = geo.ksplit > 1 && g_t64_mode != 15 ? t64_tickets(geo.row_tiles, (long long)geo.ksplit * n * m * 4) : nullptr;
+  const int pstore = (long long)geo.ksplit * n * m * 4 <= 0x7FFFFFFFLL ? g_t64_pstore : 0;
   auto lab = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc, ws,
-                       geo.ksplit, geo.kc, tickets);
+                       geo.ksplit, geo.kc, tickets, pstore);
   };
   if (g_t64_mode >= 16 && nested) {                          // lab ablations (nested bf16 / fp16 only)
     switch (g_t64_mode - 16) {
@@ -575,10 +583,10 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
     }
   } else if (nested)
     hipLaunchKernelGGL((k_gemm_4bit_t64<T, true>), grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb,
-                       st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets);
+                       st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
   else
     hipLaunchKernelGGL((k_gemm_4bit_t64<T, false>), grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B,
-                       ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets);
+                       ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
   if (geo.ksplit > 1 && g_t64_mode != 15 && tickets == nullptr)
     launch_splitk_rows_reduce<T>(ws, geo.ksplit, n, m, out, ldc);
   return true;
@@ -601,6 +609,13 @@ int cgemm_4bit_set_t64_splits(int ks) {                   // [lab] force the spl
 }
 // [additive, testing] split-K combine of the 33..64-token kernel: 1 = in the kernel (last workgroup of each row tile),
 // 0 (default) = the separate reduce launch; returns the previous setting
+// [additive, testing] partial-store policy of that kernel's split-K: 0 plain, 1 write-through dwords, 2 (default)
+// write-through 16-B lines staged through LDS; returns the previous setting
+int cgemm_4bit_set_t64_pstore(int p) {
+  const int prev = bnb::g_t64_pstore;
+  bnb::g_t64_pstore = p;
+  return prev;
+}
 int cgemm_4bit_set_t64_combine(int on) {
   const int prev = bnb::g_t64_combine;
   bnb::g_t64_combine = on ? 1 : 0;

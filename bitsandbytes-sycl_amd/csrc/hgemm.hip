@@ -795,7 +795,10 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
           const int n = nb + 16 * j;
           const uint32_t off = (m < M && n < N) ? rowoff + 4u * (uint32_t)n : 0x80000000u;
           // straight from the accumulator AGPRs (stores take AGPR data on gfx950): no VGPRs, no reads to schedule
-          asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" : : "a"(acc[j][i]), "v"(off), "s"(wr) : "memory");
+          if constexpr ((V & HG_V_CWT) != 0)             // write-through: no dirty partials for the reduce's boundary
+            asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen sc1" : : "a"(acc[j][i]), "v"(off), "s"(wr) : "memory");
+          else
+            asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" : : "a"(acc[j][i]), "v"(off), "s"(wr) : "memory");
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -1019,14 +1022,19 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
     pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, false, full_only);      // no (large enough) workspace: no split
   if (g_hgemm_variant == 1) {
     hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
-  } else if (pl.wi == 8 && pl.wj == 8 && pl.splits == 1 && g_hg_cwt) {
+  } else if (pl.wi == 8 && pl.wj == 8 && g_hg_cwt) {
     hgemm_launch_shape<OP, HG_V | HG_V_CWT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws,
                                                   side);
   } else if (pl.wi == 8 && pl.wj == 8) {
     hgemm_launch_shape<OP, HG_V, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
   } else if constexpr (FP) {
-    if (pl.wi == 8) hgemm_launch_shape<OP, HG_V, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-    else hgemm_launch_shape<OP, HG_V, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+    if (g_hg_cwt) {
+      if (pl.wi == 8) hgemm_launch_shape<OP, HG_V | HG_V_CWT, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+      else hgemm_launch_shape<OP, HG_V | HG_V_CWT, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+    } else {
+      if (pl.wi == 8) hgemm_launch_shape<OP, HG_V, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+      else hgemm_launch_shape<OP, HG_V, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+    }
   }
   if constexpr (FP) {
     using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
@@ -1136,8 +1144,8 @@ void chgemm_tn_plan(int m, int n, int k, int* out) {
   out[3] = pl.kchunk;
 }
 // [additive, testing] the side dequantise's A/B bits (HgSide::mode); returns the previous setting
-// [additive, testing] 1 (default): the 256 x 256 k_hgemm stores C write-through (sc1), 0: write-back; returns the
-// previous setting
+// [additive, testing] 1 (default): k_hgemm stores C and its split-K partials write-through (sc1), 0: write-back;
+// returns the previous setting
 int chgemm_set_c_store(int wt) {
   const int prev = bnb::g_hg_cwt;
   bnb::g_hg_cwt = wt ? 1 : 0;

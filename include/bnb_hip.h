@@ -253,6 +253,9 @@ int cgemm_4bit_set_t64_mode(int mode);
  * partials, vmcnt(0) + barrier, then a ticket; splits summed in order), 0 (default) = a separate reduce launch (faster:
  * DESIGN.md §4); returns the previous setting */
 int cgemm_4bit_set_t64_combine(int on);
+/* [additive, testing] that kernel's split-K partial stores: 0 = write-back, 1 = write-through dwords, 2 (default) =
+ * write-through 16-B lines staged through LDS; returns the previous setting */
+int cgemm_4bit_set_t64_pstore(int p);
 /* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
  * grid_cap = at most that many workgroups (0 = none); returns the previous p */
 int cdequantize_set_stream_cfg(int p, int grid_cap);
@@ -261,8 +264,8 @@ int cdequantize_set_stream_cfg(int p, int grid_cap);
 int cdequantize_set_store_policy(int policy);
 /* [additive, testing] k_hgemm side-dequantise A/B bits (chgemm_tn_pf_*); returns the previous value */
 int chgemm_set_side_mode(int v);
-/* [additive, testing] 1 (default): the 256 x 256 k_hgemm stores C write-through (device scope), 0: write-back;
- * returns the previous setting */
+/* [additive, testing] 1 (default): k_hgemm stores C and its split-K partials write-through (device scope), 0:
+ * write-back; returns the previous setting */
 int chgemm_set_c_store(int wt);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);

@@ -87,7 +87,7 @@ def test_t64_is_the_default_at_33_to_64_rows(dev):
                                  (57, 3584, 8192), (48, 520, 4096)])
 @pytest.mark.parametrize("splits", [0, 3, 11])
 def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
-    """The split-K partials summed by each row tile's last workgroup to finish (agent-scope release / acquire
+    """Write-through partial stores (dwords, staged 16-B lines) equal plain ones bit for bit.  The split-K partials summed by each row tile's last workgroup to finish (agent-scope release / acquire
     hand-off, one ticket per row tile) equal the separate k_skinny_reduce launch bit for bit: same additions in split
     order; whole float4 rows (N % 4 == 0, partial last row tile) and the scalar form (N = 193); more than 8 splits
     (the batched loads' second round).  Ten launches in a row and a HIP-graph replay: every ticket is back at zero
@@ -100,11 +100,16 @@ def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
     prev_ks = F.lib.cgemm_4bit_set_t64_splits(ct.c_int(splits))
     prev_mode = F.lib.cgemm_4bit_set_t64_mode(ct.c_int(2))
+    prev_ps = F.lib.cgemm_4bit_set_t64_pstore(ct.c_int(0))
     try:
         F.lib.cgemm_4bit_set_t64_combine(ct.c_int(0))
-        ref_out = F.gemm_4bit(X, q, st)
+        ref_out = F.gemm_4bit(X, q, st)                 # plain partials + the reduce launch
+        outs = []
+        for ps in (1, 2):                               # write-through partials (dwords / staged 16-B lines)
+            F.lib.cgemm_4bit_set_t64_pstore(ct.c_int(ps))
+            outs.append(F.gemm_4bit(X, q, st))
         F.lib.cgemm_4bit_set_t64_combine(ct.c_int(1))
-        outs = [F.gemm_4bit(X, q, st) for _ in range(10)]
+        outs += [F.gemm_4bit(X, q, st) for _ in range(10)]
         out = torch.empty_like(ref_out)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -123,6 +128,7 @@ def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
             replays.append(out.clone())
     finally:
         F.lib.cgemm_4bit_set_t64_combine(ct.c_int(0))
+        F.lib.cgemm_4bit_set_t64_pstore(ct.c_int(prev_ps))
         F.lib.cgemm_4bit_set_t64_mode(ct.c_int(prev_mode))
         F.lib.cgemm_4bit_set_t64_splits(ct.c_int(prev_ks))
     for o in outs + replays:

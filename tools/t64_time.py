@@ -13,6 +13,9 @@ import python_src_quants.functional as F  # noqa: E402
 import bench  # noqa: E402
 
 dev = torch.device("cuda", 0)
+# arm -> (t64 mode, in-kernel combine, partial-store policy)
+ARMS = {"t64": (0, 0, 0), "t64_pstore_wt_dword": (0, 0, 1), "t64_pstore_wt_lines": (0, 0, 2),
+        "t64_combine": (0, 1, 0), "skinny": (1, 0, 0)}
 shapes = [(11008, 4096), (4096, 11008), (4096, 4096)]
 for N, K in shapes:
     g = torch.Generator(device=dev).manual_seed(1)
@@ -25,13 +28,14 @@ for N, K in shapes:
         outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in copies]
         res = {}
         for rnd in range(3):                                  # interleaved rounds, median
-            for arm, (mode, comb) in {"t64": (0, 1), "t64_reduce_launch": (0, 0), "skinny": (1, 1)}.items():
+            for arm, (mode, comb, ps) in ARMS.items():
                 F.lib.cgemm_4bit_set_t64_mode(ct.c_int(mode))
                 F.lib.cgemm_4bit_set_t64_combine(ct.c_int(comb))
+                F.lib.cgemm_4bit_set_t64_pstore(ct.c_int(ps))
                 calls = [(lambda q=q, s=s, o=o: F.gemm_4bit(X, q, s, out=o)) for (q, s), o in zip(copies, outs)]
                 res.setdefault(arm, []).append(bench._time_graph(calls, 10) * 1e6)
         F.lib.cgemm_4bit_set_t64_mode(ct.c_int(0))
-        F.lib.cgemm_4bit_set_t64_combine(ct.c_int(1))
+        F.lib.cgemm_4bit_set_t64_combine(ct.c_int(0))
+        F.lib.cgemm_4bit_set_t64_pstore(ct.c_int(0))
         med = {a: sorted(v)[1] for a, v in res.items()}
-        print(f"{N}x{K} rows {M}: t64 (in-kernel combine) {med['t64']:.2f} us   t64 + reduce launch "
-              f"{med['t64_reduce_launch']:.2f} us   previous (skinny) {med['skinny']:.2f} us", flush=True)
+        print(f"{N}x{K} rows {M}: " + "   ".join(f"{a} {v:.2f} us" for a, v in med.items()), flush=True)
