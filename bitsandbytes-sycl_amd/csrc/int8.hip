@@ -291,10 +291,16 @@ k_double_rowcol_quant_wide(const fp16_t* __restrict__ A, const float* __restrict
 // half of kDoubleRowColQuant, 3384-3512) with the same expressions -- rowStats = max |a| (or the
 // -50000 the callers pre-fill when a row has no finite |a|), CA = rint(a * (127 / rowStats)).
 constexpr int RQ_MAX_VEC = 32;   // 16-B vectors per lane: K <= 16384
+typedef uint32_t rq_u32x2_t __attribute__((ext_vector_type(2)));
+// cint8_set_row_quant_store; off: measured neutral (row quantise 30.5 vs 30.7 us, + igemmlt 156.7 vs 156.8 us at
+// 4096 x 11008; the 90 MB fp16 read, not the 45 MB int8 write, sets its time; profiles/lab/r04_store_policy.txt)
+static int g_rq_wt = 0;
 
 // NV = 16-B vectors per lane (the smallest instance that holds the row: registers decide how many rows a CU keeps in
 // flight -- 32 vectors cost 171 VGPRs, two waves per SIMD)
-template <int NV>
+// WT: the int8 row stores write-through (device scope), so the GEMM launch that reads CA next inherits no dirty L2
+// lines to write back at its boundary (cint8_set_row_quant_store)
+template <int NV, bool WT = false>
 __global__ void __launch_bounds__(256)
 k_row_quant(const fp16_t* __restrict__ A, float* __restrict__ rowStats, int8_t* __restrict__ out, int rows, int cols) {
   const int lane = threadIdx.x & 63;
@@ -333,7 +339,10 @@ k_row_quant(const fp16_t* __restrict__ A, float* __restrict__ rowStats, int8_t* 
         const float a = (float)__builtin_bit_cast(fp16_t, (uint16_t)(w[j >> 1] >> (16 * (j & 1))));
         q[j >> 2] |= (uint32_t)(uint8_t)rint_i8(__fmul_rn(a, rsc)) << (8 * (j & 3));
       }
-      dst[c] = make_uint2(q[0], q[1]);
+      if constexpr (WT)
+        asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(dst + c), "v"((rq_u32x2_t){q[0], q[1]}) : "memory");
+      else
+        dst[c] = make_uint2(q[0], q[1]);
     }
   }
 }
@@ -691,19 +700,26 @@ int cint8_row_quant_fp16(fp16_t* A, float* rowStats, char* out_row, int rows, in
   if (rows <= 0 || cols <= 0) return 0;
   if (cols % 8 || cols > 64 * 8 * RQ_MAX_VEC || ((uintptr_t)A & 15) || ((uintptr_t)out_row & 7)) return 1;
   const int per_lane = (cols / 8 + 63) / 64;
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((rows + 3) / 4), dim3(256), 0, current_stream(), A, rowStats, (int8_t*)out_row, rows,
-                       cols);
+  auto go = [&](auto kern, auto kern_wt) {
+    hipLaunchKernelGGL(g_rq_wt ? kern_wt : kern, dim3((rows + 3) / 4), dim3(256), 0, current_stream(), A, rowStats,
+                       (int8_t*)out_row, rows, cols);
   };
-  if (per_lane <= 4) go(k_row_quant<4>);
-  else if (per_lane <= 8) go(k_row_quant<8>);
-  else if (per_lane <= 12) go(k_row_quant<12>);
-  else if (per_lane <= 16) go(k_row_quant<16>);
-  else if (per_lane <= 22) go(k_row_quant<22>);   // K = 11008: 22 vectors, 4 waves per SIMD
-  else if (per_lane <= 24) go(k_row_quant<24>);
-  else go(k_row_quant<RQ_MAX_VEC>);
+  if (per_lane <= 4) go(k_row_quant<4>, k_row_quant<4, true>);
+  else if (per_lane <= 8) go(k_row_quant<8>, k_row_quant<8, true>);
+  else if (per_lane <= 12) go(k_row_quant<12>, k_row_quant<12, true>);
+  else if (per_lane <= 16) go(k_row_quant<16>, k_row_quant<16, true>);
+  else if (per_lane <= 22) go(k_row_quant<22>, k_row_quant<22, true>);   // K = 11008: 22 vectors, 4 waves per SIMD
+  else if (per_lane <= 24) go(k_row_quant<24>, k_row_quant<24, true>);
+  else go(k_row_quant<RQ_MAX_VEC>, k_row_quant<RQ_MAX_VEC, true>);
   BNB_LAUNCH_CHECK("int8_row_quant");
   return 0;
+}
+
+// [additive, testing] 1: cint8_row_quant_fp16 stores CA write-through (device scope), 0: write-back; returns the previous
+int cint8_set_row_quant_store(int wt) {
+  const int prev = bnb::g_rq_wt;
+  bnb::g_rq_wt = wt ? 1 : 0;
+  return prev;
 }
 
 void cdouble_rowcol_quant(fp16_t* A, float* rowStats, float* colStats, char* out_col_normed, char* out_row_normed,

@@ -166,6 +166,9 @@ void cget_col_row_stats(bnb_fp16* A, float* rowStats, float* colStats, int* nnz_
  * inference forward (no CAt needed).  Returns 0 when launched, 1 when the shape needs the two-kernel path
  * (cols % 8, cols > 16384, unaligned pointers). */
 int cint8_row_quant_fp16(bnb_fp16* A, float* rowStats, char* out_row, int rows, int cols);
+/* [additive, testing] 1: cint8_row_quant_fp16 stores CA write-through (device scope), 0: write-back; returns the
+ * previous setting */
+int cint8_set_row_quant_store(int wt);
 void cdouble_rowcol_quant(bnb_fp16* A, float* rowStats, float* colStats, char* out_col_normed, char* out_row_normed,
                           int* rowidx, int* colidx, bnb_fp16* val, int* nnz_row_ptr, float threshold, int rows,
                           int cols);                                                             /* :338 */
