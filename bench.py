@@ -138,6 +138,20 @@ def bench_int8(dev, m, n, k, iters=50):
             "reference_abi_path": abi}
 
 
+def auto_chunks(world, requested=0):
+    """Token-row chunks of the sharded step (their all-gathers overlap the next chunk's GEMM).  Two chunks hide at most
+    half the gather but run the rank's GEMM as two half-height products, which costs more compute the narrower the
+    shard (tools/shard_parts_probe.py, profiles/lab/r04_shard_compute.txt: dequantise + GEMM per rank 156.6 vs 239.8 us
+    at world 2, 105.6 vs 147.5 at 4, 66.7 vs 126.5 at 8 for one vs two chunks).  Chunking pays while half the gather
+    exceeds that extra: with the per-peer xGMI bound of SURVEY §8(e) (~16.8 / 8.4 / 4.2 MB per link) the gather is
+    ~220 / ~110 / ~55 us at 2 / 4 / 8 GPUs -- two chunks at 2 and 4, one at 8."""
+    if world <= 1:
+        return 1
+    if requested >= 1:
+        return requested if M % requested == 0 else 1
+    return 1 if world >= 8 else 2
+
+
 def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
     """The metric's INT8 half at 1/2/4/8 GPUs: Linear8bitLt's CB/SCB [n, k] sharded by output
     feature (ColumnShardedLinear8bitLt, rows of CB), the fp16 activations replicated and row-quantised on every
@@ -766,8 +780,9 @@ def main():
     ap.add_argument("--prewarm-ms", type=float, default=400.0, help="untimed clock-ramp period before warmup")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 ranks on one GPU")
-    ap.add_argument("--chunks", type=int, default=2,
-                    help="N>1: token-row chunks whose all-gathers overlap the next chunk's GEMM")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="N>1: token-row chunks whose all-gathers overlap the next chunk's GEMM (0 = auto: 2 at 2 and "
+                         "4 GPUs, 1 at 8 -- see auto_chunks)")
     args = ap.parse_args()
     PREFETCH[0] = args.prefetch
 
@@ -798,7 +813,7 @@ def main():
         q = q.clone()
         del q_full
     Y = torch.empty(M, shard, device=dev, dtype=torch.bfloat16)
-    chunks = args.chunks if (world > 1 and args.chunks >= 1 and M % args.chunks == 0) else 1
+    chunks = auto_chunks(world, args.chunks)
     Mc = M // chunks
     gathered = torch.empty(chunks, world, Mc, shard, device=dev, dtype=torch.bfloat16) if world > 1 else None
     # N > 1: the step ends with the layer's [M, N] output assembled (chunk by chunk, as each gather lands)
