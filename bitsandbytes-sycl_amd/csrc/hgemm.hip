@@ -198,16 +198,31 @@ __device__ __forceinline__ void hg_static_for(F&& f) {
 }
 
 template <int WI, int WJ> struct HgPlan3;
+// (lab: tools/hgemm_plan_sweep.sh builds the lab with these positions moved -- HG_P3_DB1 / DB2 / DB3 shift barrier B1 /
+// B2 / B3 and everything keyed to it; the library is built with all three 0)
+#ifndef HG_P3_DB1
+#define HG_P3_DB1 0
+#endif
+#ifndef HG_P3_DB2
+#define HG_P3_DB2 0
+#endif
+#ifndef HG_P3_DB3
+#define HG_P3_DB3 0
+#endif
 template <> struct HgPlan3<8, 8> {
-  static constexpr int B1 = 21, B2 = 50, B3 = 88, SETB = 22, SETA = 61, VM = 13, SIDEQ = 120;
+  static constexpr int D1 = HG_P3_DB1, D2 = HG_P3_DB2, D3 = HG_P3_DB3;
+  static constexpr int B1 = 21 + D1, B2 = 50 + D2, B3 = 88 + D3, SETB = 22 + D1, SETA = 61 + D2, VM = 13, SIDEQ = 120;
   __host__ __device__ static constexpr int wread(int q) { return q < 16 && (q & 1) == 0 ? q >> 1 : -1; }
-  __host__ __device__ static constexpr int xread(int q) { return q >= 23 && q <= 44 && (q - 23) % 3 == 0 ? (q - 23) / 3 : -1; }
+  __host__ __device__ static constexpr int xread(int q) {
+    return q >= 23 + D1 && q <= 44 + D1 && (q - 23 - D1) % 3 == 0 ? (q - 23 - D1) / 3 : -1;
+  }
   __host__ __device__ static constexpr int bpiece(int q) {
-    return q == 24 ? 0 : q == 28 ? 1 : q == 32 ? 2 : q == 36 ? 3 : q == 40 ? 4 : q == 52 ? 5 : q == 56 ? 6 : q == 60 ? 7 : -1;
+    return q == 24 + D1 ? 0 : q == 28 + D1 ? 1 : q == 32 + D1 ? 2 : q == 36 + D1 ? 3 : q == 40 + D1 ? 4
+         : q == 52 + D2 ? 5 : q == 56 + D2 ? 6 : q == 60 + D2 ? 7 : -1;
   }
   __host__ __device__ static constexpr int apiece(int q) {
-    return q == 64 ? 0 : q == 68 ? 1 : q == 72 ? 2 : q == 76 ? 3 : q == 80 ? 4 : q == 97 ? 5 : q == 107 ? 6
-                                                                                                        : q == 117 ? 7 : -1;
+    return q == 64 + D2 ? 0 : q == 68 + D2 ? 1 : q == 72 + D2 ? 2 : q == 76 + D2 ? 3 : q == 80 + D2 ? 4
+         : q == 97 + D3 ? 5 : q == 107 + D3 ? 6 : q == 117 + D3 ? 7 : -1;
   }
   __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 31 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
 };
