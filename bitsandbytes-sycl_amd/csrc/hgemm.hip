@@ -209,6 +209,9 @@ template <int WI, int WJ> struct HgPlan3;
 #ifndef HG_P3_DB3
 #define HG_P3_DB3 0
 #endif
+#ifndef HG_P3_ABL
+#define HG_P3_ABL 0
+#endif
 template <> struct HgPlan3<8, 8> {
   static constexpr int D1 = HG_P3_DB1, D2 = HG_P3_DB2, D3 = HG_P3_DB3;
   static constexpr int B1 = 21 + D1, B2 = 50 + D2, B3 = 88 + D3, SETB = 22 + D1, SETA = 61 + D2, VM = 13, SIDEQ = 120;
@@ -641,8 +644,9 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       if constexpr (P3::wread(q) >= 0) w1[P3::wread(q)] = rd(st, wo1, P3::wread(q));
       if constexpr (P3::xread(q) >= 0) x1[P3::xread(q)] = rd(st, xo1, P3::xread(q));
       if constexpr (q == P3::B1 || q == P3::B2) {
-        __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0)
-        if constexpr (!L) __builtin_amdgcn_s_barrier();
+        // (HG_P3_ABL, lab builds only -- races, wrong results, timing only: 1 = no barrier at B1 / B2, 2 = no wait)
+        if constexpr ((HG_P3_ABL & 2) == 0) __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0)
+        if constexpr (!L && (HG_P3_ABL & 1) == 0) __builtin_amdgcn_s_barrier();
       }
       if constexpr (!L) {
         if constexpr (q == P3::SETB) hg_set_m0(ldsB0 + st * STG);
