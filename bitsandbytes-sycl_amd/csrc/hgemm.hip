@@ -654,9 +654,12 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
         if constexpr (q == P3::SETA) hg_set_m0(ldsA0 + st * STG);
         if constexpr (P3::apiece(q) >= 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[P3::apiece(q)]);
         if constexpr (q == P3::B3) {
-          if (SIDE && sd_i1 >= 0) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM + 3) : "memory");  // (+ its 3 loads)
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM) : "memory");
-          __builtin_amdgcn_s_barrier();
+          // (HG_P3_ABL lab bits: 4 = no vmcnt wait at B3, 8 = no barrier at B3 -- timing only)
+          if constexpr ((HG_P3_ABL & 4) == 0) {
+            if (SIDE && sd_i1 >= 0) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM + 3) : "memory");  // (+ its 3 loads)
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P3::VM) : "memory");
+          }
+          if constexpr ((HG_P3_ABL & 8) == 0) __builtin_amdgcn_s_barrier();
           if constexpr (SIDE) if (sd_i2 >= 0 && !(side.mode & 8)) side_words(sd_i2);   // issued two k-tiles ago:
         }                                                                                 // covered by this wait
         if constexpr (SIDE) {                            // (3 MFMAs between the dependent LDS reads and their use)
