@@ -212,9 +212,16 @@ template <int WI, int WJ> struct HgPlan3;
 #ifndef HG_P3_ABL
 #define HG_P3_ABL 0
 #endif
+#ifndef HG_P3_AEARLY
+#define HG_P3_AEARLY 0
+#endif
 template <> struct HgPlan3<8, 8> {
   static constexpr int D1 = HG_P3_DB1, D2 = HG_P3_DB2, D3 = HG_P3_DB3;
-  static constexpr int B1 = 21 + D1, B2 = 50 + D2, B3 = 88 + D3, SETB = 22 + D1, SETA = 61 + D2, VM = 13, SIDEQ = 120;
+  // HG_P3_AEARLY (lab): the last 3 A pieces before B3 too (q B2 + 32, 34, 36), so B3 waits vmcnt(16) and the next
+  // tile's fragment-read burst carries no DMA
+  static constexpr int AE = HG_P3_AEARLY;
+  static constexpr int B1 = 21 + D1, B2 = 50 + D2, B3 = 88 + D3, SETB = 22 + D1, SETA = 61 + D2, VM = AE ? 16 : 13,
+                       SIDEQ = 120;
   __host__ __device__ static constexpr int wread(int q) { return q < 16 && (q & 1) == 0 ? q >> 1 : -1; }
   __host__ __device__ static constexpr int xread(int q) {
     return q >= 23 + D1 && q <= 44 + D1 && (q - 23 - D1) % 3 == 0 ? (q - 23 - D1) / 3 : -1;
@@ -225,7 +232,8 @@ template <> struct HgPlan3<8, 8> {
   }
   __host__ __device__ static constexpr int apiece(int q) {
     return q == 64 + D2 ? 0 : q == 68 + D2 ? 1 : q == 72 + D2 ? 2 : q == 76 + D2 ? 3 : q == 80 + D2 ? 4
-         : q == 97 + D3 ? 5 : q == 107 + D3 ? 6 : q == 117 + D3 ? 7 : -1;
+         : AE ? (q == 82 + D2 ? 5 : q == 84 + D2 ? 6 : q == 86 + D2 ? 7 : -1)
+              : (q == 97 + D3 ? 5 : q == 107 + D3 ? 6 : q == 117 + D3 ? 7 : -1);
   }
   __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 31 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
 };
@@ -641,8 +649,11 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       } else {
         acc[j][i] = Op::mma(w1[j], x1[i], acc[j][i]);
       }
-      if constexpr (P3::wread(q) >= 0) w1[P3::wread(q)] = rd(st, wo1, P3::wread(q));
-      if constexpr (P3::xread(q) >= 0) x1[P3::xread(q)] = rd(st, xo1, P3::xread(q));
+      // (HG_P3_ABL lab bits, timing only: 16 = no LDS-DMA pieces in the loop, 32 = no fragment reads in the loop)
+      if constexpr ((HG_P3_ABL & 32) == 0) {
+        if constexpr (P3::wread(q) >= 0) w1[P3::wread(q)] = rd(st, wo1, P3::wread(q));
+        if constexpr (P3::xread(q) >= 0) x1[P3::xread(q)] = rd(st, xo1, P3::xread(q));
+      }
       if constexpr (q == P3::B1 || q == P3::B2) {
         // (HG_P3_ABL, lab builds only -- races, wrong results, timing only: 1 = no barrier at B1 / B2, 2 = no wait)
         if constexpr ((HG_P3_ABL & 2) == 0) __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0)
@@ -650,9 +661,9 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       }
       if constexpr (!L) {
         if constexpr (q == P3::SETB) hg_set_m0(ldsB0 + st * STG);
-        if constexpr (P3::bpiece(q) >= 0) glds16_chain<1024>(B + (long long)kn * 128, boff[P3::bpiece(q)]);
+        if constexpr (P3::bpiece(q) >= 0 && (HG_P3_ABL & 16) == 0) glds16_chain<1024>(B + (long long)kn * 128, boff[P3::bpiece(q)]);
         if constexpr (q == P3::SETA) hg_set_m0(ldsA0 + st * STG);
-        if constexpr (P3::apiece(q) >= 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[P3::apiece(q)]);
+        if constexpr (P3::apiece(q) >= 0 && (HG_P3_ABL & 16) == 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[P3::apiece(q)]);
         if constexpr (q == P3::B3) {
           // (HG_P3_ABL lab bits: 4 = no vmcnt wait at B3, 8 = no barrier at B3 -- timing only)
           if constexpr ((HG_P3_ABL & 4) == 0) {
@@ -678,7 +689,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
           }
           if constexpr (q == P3::SIDEQ) if (sd_go && sd_it < side.iters) side_issue();
         }
-        constexpr int r = P3::nread(q);                  // w0[0], x0[0..WI-1], w0[1..WJ-1]: the order of their use
+        constexpr int r = (HG_P3_ABL & 32) ? -1 : P3::nread(q);   // w0[0], x0[0..WI-1], w0[1..WJ-1]: their use order
         if constexpr (r == 0) w0[0] = rd(st ^ 1, wo0, 0);
         else if constexpr (r > 0 && r <= WI) x0[r - 1] = rd(st ^ 1, xo0, r - 1);
         else if constexpr (r > WI) w0[r - WI] = rd(st ^ 1, wo0, r - WI);
