@@ -1,7 +1,9 @@
 """Benchmark: NF4 matmul TFLOPS (+ INT8 igemmlt TOPS) @ M=4096, N=4096, K=11008 on 1..8 MI355X.
 
-A "step" = one pass of the hot path over one batch of synthetic input:
-    nested-absmax dequant (fp32) -> fused NF4 GEMM  Y_r = X @ W_r^T  (bf16, MFMA)
+A "step" = one pass of the hot path over one batch of synthetic input, through functional.gemm_4bit as
+MatMul4Bit.forward calls it (ref:python_src_quants/autograd/_functions.py:507):
+    k_dequantize_4bit_stream (NF4 -> bf16 weight, nested statistics decoded in the same launch)
+    -> the hand-written bf16 GEMM k_hgemm  Y_r = X @ W_r^T  (MFMA)
     -> RCCL all-gather of the bf16 output shards (when --gpus > 1).
 W [4096, 11008] is column-sharded by output feature across ranks (rank r owns rows
 r*N/g .. (r+1)*N/g of W, quantised NF4 bs=64 with nested statistics, the Linear4bit
@@ -12,6 +14,7 @@ Prints ONE JSON line on rank 0 (driver contract).  Extra fields: int8 igemmlt TO
 dequantize GB/s, the roofline of the dominant kernel and the CPU baseline.
 
 Launch:  python bench.py [--gpus 1 --steps 20 --warmup 5]
+         python bench.py --gpus N        (N > 1, no launcher: starts N rank processes itself, see launch_ranks)
          python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
@@ -20,6 +23,7 @@ import argparse
 import ctypes as ct
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -27,6 +31,61 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "bitsandbytes-sycl_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
+
+
+def _gpus_arg(argv) -> int:
+    """--gpus N / --gpus=N from the command line (1 when absent); nothing else is parsed here."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    return ap.parse_known_args(argv)[0].gpus
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(argv, port: int) -> list:
+    """The command that runs this bench as `gpus` rank processes on this node (one per GPU, torch.distributed.run on
+    127.0.0.1, the same arguments) -- what the driver's N > 1 launch line does."""
+    n = _gpus_arg(argv)
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def world_mismatch(argv, env) -> str:
+    """A message when the launcher's WORLD_SIZE and --gpus disagree (the bench would otherwise measure a world size
+    other than the one it reports), else ''."""
+    if "WORLD_SIZE" not in env:
+        return ""
+    world, gpus = int(env["WORLD_SIZE"]), _gpus_arg(argv)
+    if world != gpus:
+        return (f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {gpus}: launch {gpus} ranks "
+                f"(--nproc-per-node {gpus}) or pass --gpus {world}")
+    return ""
+
+
+def launch_ranks(argv) -> None:
+    """--gpus N > 1 without a launcher (no WORLD_SIZE): start the N rank processes as ONE child (torch.distributed.run,
+    so each rank gets RANK / LOCAL_RANK / WORLD_SIZE and its own GPU) and exit with its status -- before this process
+    touches the GPU or imports torch, so nothing here has initialised HIP when the child starts.  Rank 0 of the child
+    prints the JSON line.  A WORLD_SIZE that disagrees with --gpus exits non-zero (see world_mismatch)."""
+    msg = world_mismatch(argv, os.environ)
+    if msg:
+        print(msg, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if "WORLD_SIZE" in os.environ or _gpus_arg(argv) <= 1:
+        return
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    rc = subprocess.call(rank_launch_cmd(argv, _free_port()), env=env)
+    sys.exit(rc)
+
+
+if __name__ == "__main__":
+    launch_ranks(sys.argv[1:])
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -783,12 +842,31 @@ def main():
     ap.add_argument("--chunks", type=int, default=0,
                     help="N>1: token-row chunks whose all-gathers overlap the next chunk's GEMM (0 = auto: 2 at 2 and "
                          "4 GPUs, 1 at 8 -- see auto_chunks)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="print the rank layout (every rank over gloo, no GPU work) and exit: checks the N-rank launch")
     args = ap.parse_args()
     PREFETCH[0] = args.prefetch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:       # (launch_ranks has already started the ranks / refused a mismatch; imported callers)
+        raise SystemExit(world_mismatch(sys.argv[1:], os.environ) or
+                         f"bench.py: world size {world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        # the rank layout only (no GPU): every rank joins a gloo group and rank 0 prints who took part
+        if world > 1:
+            dist.init_process_group("gloo")
+        ranks = [None] * world
+        if world > 1:
+            dist.all_gather_object(ranks, {"rank": rank, "local_rank": local_rank, "pid": os.getpid()})
+        else:
+            ranks = [{"rank": 0, "local_rank": local_rank, "pid": os.getpid()}]
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "gpus_arg": args.gpus, "ranks": ranks}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if world > 1:
@@ -971,14 +1049,11 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (seeded randn; W ~ N(0,0.02) -> NF4 bs=64 nested stats; X ~ N(0,1) bf16)",
-            "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (functional.gemm_4bit: HIP "
-                                   "dequantise + the hand-written bf16 GEMM k_hgemm at this M"
+            "config": {"workload": "NF4 Linear4bit GEMM M=4096 N=4096 K=11008 (functional.gemm_4bit on its static "
+                                   f"route for {Mc} x {shard} x {K}: {kname}"
                                    + ("; the dequantise of each step's weight run inside the previous step's k_hgemm "
                                       "(--prefetch)" if PREFETCH[0] else ", every step dequantising its weight") +
-                                   "; fused dequant+MFMA "
-                                   f"kernel below {F.GEMM_4BIT_DEQUANT_MIN_ROWS} rows / "
-                                   f"{F.GEMM_4BIT_DEQUANT_MIN_FEATURES} features) + bf16 all-gather of output-column "
-                                   "shards",
+                                   ")" + (" + bf16 all-gather of output-column shards" if world > 1 else ""),
                        "M": M, "N": N, "K": K, "blocksize": BS, "quant_type": "nf4", "compress_statistics": True,
                        "parallelism": (f"column-shard x{world} + RCCL all_gather, {chunks} token-row chunks "
                                        "(chunk c's all-gather overlaps chunk c+1's GEMM; the step ends with the [M, N] "

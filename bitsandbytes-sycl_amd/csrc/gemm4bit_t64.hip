@@ -470,11 +470,15 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     volatile uint32_t* last = reinterpret_cast<volatile uint32_t*>(sm);   // the table: no DMA is in flight any more
+    // (the ticket is acquire-release at agent scope and the last arriver's waves take an agent acquire before reading:
+    // the hand-off then rests on the memory model, not only on the sc1 cache policy of the partial stores and loads --
+    // ADVICE r4; opt-in path, so its cost (a cache-wide write-back / invalidate per workgroup) is accepted)
     if (tid == 0)
-      last[0] = __hip_atomic_fetch_add(&tickets[rt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+      last[0] = __hip_atomic_fetch_add(&tickets[rt], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
                 (uint32_t)(ksplit - 1) ? 1u : 0u;
     __syncthreads();
     if (last[0] == 0u) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     t64_combine<T>(wsr, ksplit, M, N, rt * T64_ROWS, out, ldc, tid);
     if (tid == 0) __hip_atomic_store(&tickets[rt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -498,9 +502,16 @@ int g_t64_combine = 0;
 // 22.3, 4096^2 19.0 -> 15.5; write-through dwords within 0.2 us of the lines; profiles/lab/r04_t64.txt)
 int g_t64_pstore = 2;
 
-// this launch's ticket set on the current device (nullptr: use the reduce launch)
+// this launch's ticket set on the current device (nullptr: use the reduce launch).  Never during HIP-graph capture: a
+// captured launch would bake one ticket set into the graph, and its replays could then share counters with eager
+// launches handed the same set -- captured work always takes the reduce launch.
 static uint32_t* t64_tickets(int row_tiles, long long partial_bytes) {
   if (!g_t64_combine || row_tiles > T64_MAX_TILES || partial_bytes > 0x7FFFFFFFLL) return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(current_stream(), &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
   static uint32_t* base[64] = {};
   static unsigned next[64] = {};
   int dev = 0;

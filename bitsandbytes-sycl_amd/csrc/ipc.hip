@@ -18,6 +18,10 @@
 // epoch (state[0], this rank's own device word) counts the steps, parity p = epoch & 1: a rank can only push parity p
 // of step e + 2 after it saw every peer's step e + 1 flag, i.e. after every peer's stream finished step e's copy-out,
 // so two parities suffice.  Kernels of one rank run in stream order, so state[0] needs no atomics.
+// Failure is fail-stop: a step whose wait timed out writes NaN (0xFFFF in every 16-bit element, NaN in bf16 and fp16)
+// to `rows` instead of the slots, whose contents are then stale; the timeout count state[1] is sticky, and every later
+// step of this exchange only writes the NaN row (no push, no epoch advance) -- so the peers time out in turn and a lost
+// rank never yields a silently wrong row on any rank.  The host reads state[1] (IpcAllGather.timeouts / check).
 #include "common.hpp"
 
 #include <cstring>
@@ -42,9 +46,20 @@ __device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
 __global__ void __launch_bounds__(256)
 k_ipc_allgather_push(const unsigned long long* __restrict__ bufs, int rank, int world, long long slot_bytes,
                      const uint4* __restrict__ y, long long y_pieces, uint4* __restrict__ rows, unsigned* __restrict__ state) {
+  __shared__ int s_fail;
+  const int tid = threadIdx.x;
+  const long long row_pieces = (long long)world * y_pieces;
+  auto poison = [&]() {
+    for (long long i = tid; i < row_pieces; i += blockDim.x) rows[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  };
+  if (tid == 0) s_fail = state[1] != 0u;
+  __syncthreads();
+  if (s_fail) {                 // latched: an earlier step timed out, the exchange is out of step for good
+    poison();
+    return;
+  }
   const unsigned e = state[0] + 1;
   const int p = e & 1;
-  const int tid = threadIdx.x;
   // 1. push this rank's slice into slot (p, rank) of every rank's buffer
   for (int j = 0; j < world; ++j) {
     uint8_t* dst = reinterpret_cast<uint8_t*>(bufs[j]) + IPC_FLAG_BYTES + ((long long)p * world + rank) * slot_bytes;
@@ -67,6 +82,7 @@ k_ipc_allgather_push(const unsigned long long* __restrict__ bufs, int rank, int 
       if (++it >= kSpinLimit) {
         state[1] += 1;          // (a racy count is fine: any non-zero value reports the failure)
         state[2] = tid + 1;
+        s_fail = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -74,14 +90,16 @@ k_ipc_allgather_push(const unsigned long long* __restrict__ bufs, int rank, int 
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (s_fail) {                 // a source never pushed this step: its slot is stale, the row is not valid
+    poison();
+    return;
+  }
   // 3. the g slots of parity p are the assembled row
   const uint8_t* own = reinterpret_cast<const uint8_t*>(bufs[rank]) + IPC_FLAG_BYTES + (long long)p * world * slot_bytes;
-  const long long slot_pieces = slot_bytes / 16;
   for (int j = 0; j < world; ++j) {
     const uint4* src = reinterpret_cast<const uint4*>(own + (long long)j * slot_bytes);
     for (long long i = tid; i < y_pieces; i += blockDim.x) rows[(long long)j * y_pieces + i] = src[i];
   }
-  (void)slot_pieces;
   __syncthreads();
   if (tid == 0) state[0] = e;
 }
@@ -96,8 +114,11 @@ long long cipc_allgather_buffer_bytes(int world, int n, int elem) {
   return bnb::IPC_FLAG_BYTES + 2LL * world * bnb::ipc_slot_bytes(n, elem);
 }
 
-// [additive] allocate a zeroed exchange buffer (uncached device memory; fine-grained, then plain hipMalloc as
-// fallbacks); *kind = 2 uncached, 1 fine-grained, 0 plain.  Returns the device pointer or NULL (cget_last_error*).
+// [additive] allocate a zeroed exchange buffer: uncached device memory (*kind = 2), else fine-grained (*kind = 1) --
+// both keep a peer's stores visible to the owner's system-scope acquire loads.  Plain coarse-grained memory is NOT a
+// fallback: the owner's L2 could serve stale lines of the slots and flags the peers write over xGMI, so the gather
+// could return an earlier step's row; when neither kind can be allocated this fails (NULL, cget_last_error*) and the
+// caller keeps the RCCL gather.
 void* cipc_alloc(long long bytes, int* kind) {
   BNB_RANGE("cipc_alloc");
   void* p = nullptr;
@@ -107,11 +128,8 @@ void* cipc_alloc(long long bytes, int* kind) {
     k = 1;
     if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained) != hipSuccess) {
       (void)hipGetLastError();
-      k = 0;
-      if (hipMalloc(&p, (size_t)bytes) != hipSuccess) {
-        bnb::set_error(2, "cipc_alloc: allocation failed");
-        return nullptr;
-      }
+      bnb::set_error(2, "cipc_alloc: neither uncached nor fine-grained device memory could be allocated");
+      return nullptr;
     }
   }
   if (hipMemset(p, 0, (size_t)bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {

@@ -875,6 +875,64 @@ def _hgemm_fits(rows: int, N: int, K: int) -> bool:
             and (rows - 1) * K * 2 + 2 * K <= 0xFFFFFFFF and (N - 1) * K * 2 + 2 * K <= 0xFFFFFFFF)
 
 
+_U32 = 0xFFFFFFFF
+
+
+def _hgemm_chunks(rows: int, N: int, K: int, blocksize: int) -> Tuple[int, int]:
+    """(row chunk, weight-row chunk) sizes for a product k_hgemm cannot take in one launch (_hgemm_fits: 32-bit lane
+    offsets).  Row chunks: the most activation rows whose offsets fit, rounded down to whole 256-row tiles.  Weight
+    chunks: the most weight rows whose bf16 copy fits the same bound and the dequantise's 32-bit element count, a
+    multiple of 256 rows and of whole statistics blocks (so every chunk starts on a block boundary)."""
+    rc = rows if (rows - 1) * K * 2 + 2 * K <= _U32 else max(256, ((_U32 - 2 * K) // (2 * K) + 1) // 256 * 256)
+    if (N - 1) * K * 2 + 2 * K <= _U32 and N * K < 2 ** 31:
+        return rc, N
+    unit = 256
+    while (unit * K) % blocksize:
+        unit *= 2
+    nc = min((_U32 - 2 * K) // (2 * K) + 1, (2 ** 31 - 1) // K) // unit * unit
+    return rc, max(unit, nc)
+
+
+def _gemm_4bit_hgemm_chunked(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor,
+                             absmax: Optional[Tensor]) -> Tensor:
+    """dequantise + k_hgemm for operands beyond one launch's 32-bit offsets (previously the library
+    GEMM): the weight is dequantised one row chunk at a time into the weight workspace, and each weight chunk is
+    multiplied with each activation row chunk straight into its [rows, columns] block of `out` (ldc = N).  Every output
+    element is one k_hgemm dot product over all of K, as in the one-launch form (the plan per chunk shape may split K
+    differently, within the GEMM tolerance)."""
+    rows, K = A2.shape
+    N = state.shape[0]
+    rc, nc = _hgemm_chunks(rows, N, K, state.blocksize)
+    am = absmax if absmax is not None else _absmax_fp32(state)
+    bs = state.blocksize
+    qt = "fp4" if state.quant_type == "fp4" else "nf4"
+    deq = getattr(lib, f"cdequantize_blockwise_{_QB[A2.dtype]}_{qt}")
+    gemm = lib.chgemm_tn_ws_bf16 if A2.dtype == torch.bfloat16 else lib.chgemm_tn_ws_fp16
+    flat = Bc.reshape(-1)
+    outv = out.view(rows, N)
+    for n0 in range(0, N, nc):
+        n1 = min(N, n0 + nc)
+        W = _dequant_workspace(A2.device, A2.dtype, (n1 - n0) * K).view(n1 - n0, K)
+        prev_device = pre_call(A2.device)
+        deq(get_ptr(None), get_ptr(flat[n0 * K // 2:]), get_ptr(am[n0 * K // bs:]), get_ptr(W), ct.c_int(bs),
+            ct.c_int((n1 - n0) * K))
+        _DEQ_META.pop((A2.device, A2.dtype, _stream_key(A2.device)), None)   # the workspace holds a chunk now
+        for r0 in range(0, rows, rc):
+            r1 = min(rows, r0 + rc)
+            ws_bytes = int(lib.chgemm_tn_workspace_bytes(ct.c_int32(r1 - r0), ct.c_int32(n1 - n0), ct.c_int32(K)))
+            ws = _gemm_workspace(A2.device, ws_bytes)
+            rc_ = gemm(ct.c_int32(r1 - r0), ct.c_int32(n1 - n0), ct.c_int32(K), get_ptr(A2[r0:]), ct.c_int32(K),
+                       get_ptr(W), ct.c_int32(K), get_ptr(outv[r0:, n0:]), ct.c_int32(N), get_ptr(ws),
+                       ct.c_longlong(ws_bytes))
+            if rc_:
+                post_call(prev_device)
+                raise RuntimeError(f"bitsandbytes HIP GEMM (chgemm_tn, chunk rows {r0}:{r1} x features {n0}:{n1}) "
+                                   f"returned {rc_}: " + (lib.cget_last_error_message().decode() if rc_ == 2
+                                                          else "shape not supported"))
+        post_call(prev_device)
+    return out
+
+
 def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
     """The deterministic route of a (rows, N, K) product (round 4, tools/route_sweep4.py, profiles/lab/r04_route_sweep.txt):
       * up to GEMM_4BIT_FEW_TOKENS rows: "fused" (the few-token kernels and the multi-row GEMV, picked inside);
@@ -883,13 +941,18 @@ def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
         53-96 vs 69-100), K >= 16384 at 257..1024 rows (1024 x 28672 at 1024 rows 85 vs 102): there the bf16 weight's
         write + read costs more than the fused kernel's in-LDS dequantisation;
       * everywhere else the dequantise + the hand-written k_hgemm ("hgemm"; 256 x 256 / 256 x 128 / 128 x 256 tiles and
-        split-K by its launch plan) -- "library" only for a shape k_hgemm does not take (k % 64, 32-bit offsets)."""
+        split-K by its launch plan); operands beyond one launch's 32-bit offsets (prompts above ~195k tokens at K =
+        11008, weights above 2^31 elements) run it in row / weight chunks (_gemm_4bit_hgemm_chunked).  "library" only
+        for K % 64 != 0, which gemm_4bit does not take (gemm_4bit_supported): no vendor GEMM on the static route.
+    Accepted trade: 65..256 rows of wide weights (11008 x 4096 at 96 / 128 / 256 rows) run 5-8 % slower on
+    k_hgemm than on the library GEMM (52.5 / 54.0 / 60.4 vs 48.9 / 51.8 / 58.7 us, profiles/lab/r04_route_sweep.txt);
+    BNB_ROUTE_TUNING=1 measures and picks the faster route per shape."""
     if rows <= GEMM_4BIT_FEW_TOKENS:
         return "fused"
     if rows < GEMM_4BIT_DEQUANT_MIN_ROWS:
         if (K >= 8192 and N >= 4096 and rows <= 512) or (K >= 16384 and 256 < rows <= 1024):
             return "fused"
-    return "hgemm" if _hgemm_fits(rows, N, K) else "library"
+    return "hgemm" if K % 64 == 0 else "library"
 
 
 def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax: Optional[Tensor],
@@ -1059,7 +1122,7 @@ def _launch_prefetch_gemm(A2: Tensor, W: Tensor, out: Tensor, ws: Optional[Tenso
     else:
         stats = [an if an is not None else _absmax_fp32(sn), None, None, None, None]
         bs2 = 0
-    Bc = Bn if Bn.is_contiguous() else Bn.contiguous()
+    Bc = Bn                      # (contiguous: gemm_4bit drops the hint otherwise)
     is_on_gpu([Bc, target] + [t for t in stats if t is not None])
     fn = lib.chgemm_tn_pf_bf16 if A2.dtype == torch.bfloat16 else lib.chgemm_tn_pf_fp16
     return fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W), ct.c_int32(K),
@@ -1097,6 +1160,10 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
     if out is None:
         out = torch.empty((rows, N), dtype=A.dtype, device=A.device)
     Bc = B if B.is_contiguous() else B.contiguous()
+    if prefetch is not None and not prefetch[0].is_contiguous():
+        # the prefetched weight is matched to its consuming call by the packed bytes' pointer and version: a temporary
+        # contiguous copy would be freed at once and its address reused, so the hint needs B_next in place
+        prefetch = None
     route = gemm_4bit_static_route(rows, N, K)
     if _route is not None:
         if _route not in GEMM_4BIT_ROUTES:
@@ -1109,9 +1176,9 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
         if measured is not None:
             route = measured
     if route == "hgemm" and not _hgemm_fits(rows, N, K):
-        # a measured / imported route covers a quarter-octave of row counts: near the 32-bit offset limit the
-        # hand-written GEMM may not take these rows -- use the library GEMM instead of failing
-        route = "library"
+        # beyond one launch's 32-bit offsets: the same pair in row / weight chunks (also where a measured / imported
+        # route, which covers a quarter-octave of row counts, names "hgemm" near the limit)
+        return _gemm_4bit_hgemm_chunked(A2, Bc, state, out, absmax).view(*A.shape[:-1], N)
     library = route in ("library", "library_tn", "hgemm")
     if (not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and not _fewtok_takes(N, rows, K, state.blocksize)
             and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events)):
@@ -1195,9 +1262,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
                 if rc == 0:
                     if _PF_CUR.get(key, (None,))[0] == target:
                         _PF_CUR.pop(key, None)
-                    _PF_READY[key] = (target, _weight_meta(prefetch[0] if prefetch[0].is_contiguous()
-                                                           else prefetch[0].contiguous(), sn,
-                                                           prefetch[2] if len(prefetch) > 2 else None))
+                    _PF_READY[key] = (target, _weight_meta(prefetch[0], sn, prefetch[2] if len(prefetch) > 2 else None))
             if rc == 1:
                 fn = lib.chgemm_tn_ws_bf16 if A.dtype == torch.bfloat16 else lib.chgemm_tn_ws_fp16
                 rc = fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), get_ptr(A2), ct.c_int32(K), get_ptr(W),

@@ -290,8 +290,11 @@ class IpcAllGather:
     the prefill all-gather.  The exchange buffers live as long as this object; close() frees them after a barrier.
 
     Layout of the assembled row: rank j's columns at [j * n, (j + 1) * n) -- gathered_to_rows of the RCCL path.
-    timeouts(): polls that gave up (a peer that never pushed): 0 on a healthy step; the result of such a step is
-    not valid."""
+    Memory: every rank's exchange buffer is uncached or fine-grained device memory, and all ranks must hold the same
+    kind (setup raises otherwise -- coarse-grained memory would let the owner's L2 serve stale slots).
+    Failure is fail-stop: a step whose wait for a peer timed out writes a NaN row (never the stale slots), and so does
+    every later step of this exchange; timeouts() is the sticky count of polls that gave up (0 while healthy) and
+    check() raises when it is non-zero."""
 
     def __init__(self, n_local: int, world: int, rank: int, group=None, device=None, dtype=torch.bfloat16):
         import ctypes as ct
@@ -340,8 +343,12 @@ class IpcAllGather:
             elif err is None:
                 err = "a peer could not export its exchange buffer"
             oks = [None] * world
-            dist.all_gather_object(oks, err is None, group=group)
-            if not all(oks):
+            dist.all_gather_object(oks, (err is None, self.memory_kind), group=group)
+            kinds = {k for _, k in oks}
+            if err is None and all(ok for ok, _ in oks) and (len(kinds) != 1 or
+                                                             not kinds <= {"uncached", "fine-grained"}):
+                err = f"exchange buffers of different / unsupported memory kinds across ranks: {[k for _, k in oks]}"
+            if err is not None or not all(ok for ok, _ in oks):
                 self.close(barrier=False)
                 raise RuntimeError(f"IpcAllGather setup failed: {err or 'on a peer rank'}")
             self.table = torch.tensor(ptrs, dtype=torch.int64, device=self.device)
@@ -362,7 +369,16 @@ class IpcAllGather:
         return rows
 
     def timeouts(self) -> int:
+        """Polls that gave up so far (sticky; synchronises with the device).  Non-zero: this rank's rows have been NaN
+        since the step that timed out."""
         return int(self.state[1].item())
+
+    def check(self):
+        """Raise when any step of this exchange timed out (its rows, and every later step's, are NaN)."""
+        n = self.timeouts()
+        if n:
+            raise RuntimeError(f"IpcAllGather: {n} peer wait(s) timed out (last source rank "
+                               f"{int(self.state[2].item()) - 1}); the gathered rows are poisoned (NaN)")
 
     def close(self, barrier: bool = True):
         """Unmap the peers' buffers and free this rank's, after every rank stopped pushing (a barrier)."""
@@ -388,8 +404,12 @@ class ShardedDecode:
     [1, K] into y (ColumnShardedLinear4bit.decode_step passes the GEMV); the input goes through `set_input`."""
 
     def __init__(self, local_fn: Callable, in_features: int, n_local: int, world: int, group=None,
-                 dtype=torch.bfloat16, device=None, gather: str = "rccl", rank: Optional[int] = None):
-        self.local_fn, self.world, self.group = local_fn, world, group
+                 dtype=torch.bfloat16, device=None, gather: str = "rccl", rank: Optional[int] = None,
+                 checked: bool = False):
+        # checked (gather="ipc"): every step / replay is followed by IpcAllGather.check() -- a host synchronisation per
+        # token that turns a timed-out peer into an exception on the step that hit it (default: check() on demand, and
+        # always after capture()'s warm-up and capture)
+        self.local_fn, self.world, self.group, self.checked = local_fn, world, group, checked
         self.x = torch.zeros(1, in_features, dtype=dtype, device=device)
         self.gathered = torch.empty(world, 1, n_local, dtype=dtype, device=device)
         self.graph = None
@@ -414,11 +434,23 @@ class ShardedDecode:
     def set_input(self, x: torch.Tensor):
         self.x.copy_(x.reshape(self.x.shape))
 
+    def check(self):
+        """Raise if the IPC gather of any step so far timed out (no-op for the RCCL gather, whose errors raise)."""
+        if self.ipc is not None:
+            self.ipc.check()
+
+    def _barrier(self):
+        if self.world > 1 and dist.is_available() and dist.is_initialized():
+            dist.barrier(group=self.group)
+
     def step(self) -> torch.Tensor:
         """One eager decode step on the static buffers; returns `rows`."""
         self.local_fn(self.x, self.y)
         if self.ipc is not None:
-            return self.ipc(self.y, self.rows)
+            self.ipc(self.y, self.rows)
+            if self.checked:
+                self.ipc.check()
+            return self.rows
         if _collective(self.world):
             if dist.get_backend(self.group) == "gloo":
                 dist.all_gather(list(self.gathered.unbind(0)), self.y.clone(), group=self.group)
@@ -431,20 +463,35 @@ class ShardedDecode:
         (and leaves eager mode) when the backend cannot be captured (gloo, or a collective capture refused)."""
         if not self.x.is_cuda or (self.ipc is None and _collective(self.world) and dist.get_backend(self.group) == "gloo"):
             return False
+        # IPC: the warm-up steps wait on every peer's flags, so all ranks enter them together (a rank still loading or
+        # capturing something else could otherwise exceed the bounded wait), and their outcome is checked before the
+        # graph bakes the exchange in
+        ipc = self.ipc is not None
+        if ipc:
+            self._barrier()
         s = torch.cuda.Stream(device=self.x.device)
         s.wait_stream(torch.cuda.current_stream(self.x.device))
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self.step()
-        torch.cuda.current_stream(self.x.device).wait_stream(s)
-        torch.cuda.synchronize(self.x.device)
-        g = torch.cuda.CUDAGraph()
+        checked, self.checked = self.checked, False      # (no host sync inside the side stream / the capture)
         try:
-            with torch.cuda.graph(g):
-                self.step()
-        except Exception:  # noqa: BLE001 - capture refused: stay eager
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    self.step()
+            torch.cuda.current_stream(self.x.device).wait_stream(s)
             torch.cuda.synchronize(self.x.device)
-            return False
+            if ipc:
+                self.ipc.check()
+                self._barrier()
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g):
+                    self.step()
+            except Exception:  # noqa: BLE001 - capture refused: stay eager
+                torch.cuda.synchronize(self.x.device)
+                return False
+        finally:
+            self.checked = checked
+        if ipc:
+            self.ipc.check()
         self.graph = g
         return True
 
@@ -453,6 +500,8 @@ class ShardedDecode:
             self.set_input(x)
         if self.graph is not None:
             self.graph.replay()
+            if self.checked:
+                self.check()
             return self.rows
         return self.step()
 

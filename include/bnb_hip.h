@@ -429,9 +429,11 @@ void cdequantize_nested_absmax_fp32(float* code2, unsigned char* q, float* absma
  * cipc_allgather_buffer_bytes), exports it (cipc_get_handle), opens every peer's (cipc_open_handle), and per decode
  * step launches callgather_ipc_16: its [n] shard is pushed into every rank's buffer with an epoch flag, the rank waits
  * (bounded) for all flags and copies the assembled [world * n] row out.  state: device u32[4] zeroed once (epoch,
- * timeout count, last timed-out rank + 1). ---- */
+ * timeout count, last timed-out rank + 1).  Fail-stop: a step whose wait timed out, and every step after it, writes a
+ * NaN row (all 16-bit elements 0xFFFF) instead of stale slots; the host checks the sticky count. ---- */
 long long cipc_allgather_buffer_bytes(int world, int n, int elem);
-void* cipc_alloc(long long bytes, int* kind);   /* kind: 2 uncached, 1 fine-grained, 0 plain device memory */
+void* cipc_alloc(long long bytes, int* kind);   /* kind: 2 uncached, 1 fine-grained; NULL when neither (no
+                                                   coarse-grained fallback: peers' stores could be served stale) */
 void cipc_free(void* p);
 int cipc_handle_size(void);
 int cipc_get_handle(void* p, void* handle);

@@ -237,3 +237,57 @@ def test_fused_projections_70b_shard(dev, nested):
                 yp = (F.gemv_4bit(X, pq.t(), state=pst) if M == 1 else F.gemm_4bit(X, pq, pst)).reshape(M, -1).float()
                 r = yp.pow(2).mean().sqrt().item()
                 assert (y.float() - yp).abs().max().item() <= 4e-2 * r + 4e-2 * yp.abs().max().item()
+
+
+def test_hgemm_chunked_rows_beyond_4gib(dev):
+    """a prompt whose activations exceed one k_hgemm launch's 32-bit offsets (rows * K * 2 > 4 GiB:
+    524,588 rows x 4096) stays on the hand-written route -- row chunks of whole 256-row tiles, each multiplied straight
+    into its rows of the output -- instead of the library GEMM; sampled rows on both sides of the chunk boundary
+    against the fp64 oracle."""
+    F = _F()
+    M, N, K = 524288 + 300, 512, 4096
+    assert M * K * 2 > 2 ** 32 and not F._hgemm_fits(M, N, K)
+    assert F.gemm_4bit_static_route(M, N, K) == "hgemm"
+    rc, nc = F._hgemm_chunks(M, N, K, 64)
+    assert nc == N and rc % 256 == 0 and (rc - 1) * K * 2 + 2 * K <= 0xFFFFFFFF < M * K * 2
+    q, st = _quantized(N, K, dev, 4242)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=torch.Generator(device=dev).manual_seed(5))
+    Y = F.gemm_4bit(X, q, st)
+    rows = torch.cat([_sample_rows(M, dev, n=120, seed=9),
+                      torch.tensor([0, rc - 2, rc - 1, rc, rc + 1, M - 1], device=dev)]).unique()
+    _check_rows(Y, X, q, F._absmax_fp32(st), N, K, st.code, rows)
+    del X, Y
+    torch.cuda.empty_cache()
+
+
+def test_hgemm_chunked_weight_beyond_2g_elements(dev):
+    """A weight of more than 2^31 elements (262,400 x 8192: its bf16 copy exceeds 4 GiB) on the hand-written route:
+    dequantised one weight-row chunk at a time (whole statistics blocks), each chunk's product written into its
+    columns of the output (ldc = N).  Random packed bytes and statistics (no float weight of that size is needed);
+    sampled rows x sampled columns on both sides of the chunk boundary against the fp64 oracle on those columns."""
+    F = _F()
+    M, N, K = 2048, 262144 + 256, 8192
+    assert N * K > 2 ** 31 and not F._hgemm_fits(M, N, K)
+    assert F.gemm_4bit_static_route(M, N, K) == "hgemm"
+    rc, nc = F._hgemm_chunks(M, N, K, 64)
+    assert rc == M and nc % 256 == 0 and nc < N and nc * K < 2 ** 31
+    g = torch.Generator(device=dev).manual_seed(77)
+    q = torch.randint(0, 256, (N * K // 2, 1), device=dev, dtype=torch.uint8, generator=g)
+    am = torch.rand(N * K // 64, device=dev, generator=g) * 0.05 + 0.01
+    st = F.QuantState(absmax=am, shape=torch.Size([N, K]), code=F.get_4bit_type("nf4", device=dev), blocksize=64,
+                      quant_type="nf4", dtype=torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
+    Y = F.gemm_4bit(X, q, st)
+    cols = torch.cat([torch.randperm(N, generator=torch.Generator().manual_seed(3))[:200].to(dev),
+                      torch.tensor([0, nc - 1, nc, nc + 1, N - 1], device=dev)]).unique()
+    rows = _sample_rows(M, dev, n=64, seed=4)
+    qs = q.view(N, K // 2)[cols].contiguous()
+    ams = am.view(N, K // 64)[cols].contiguous()
+    exp = ref.gemm_4bit_dequant_ref(X[rows].float().cpu().numpy(), qs.cpu().numpy(), ams.cpu().numpy(), cols.numel(),
+                                    K, 64, st.code.cpu().numpy(), "bf16")
+    got = Y[rows][:, cols].float().cpu().numpy().astype(np.float64)
+    rms = np.sqrt(np.mean(exp ** 2))
+    err = np.abs(got - exp)
+    assert np.all(err <= 2e-2 * rms + 2e-2 * np.abs(exp)), float(err.max())
+    del X, Y, q
+    torch.cuda.empty_cache()

@@ -4,7 +4,9 @@ group, each opens the other's buffer, and every step pushes a rank-specific [1, 
 must equal the two slices side by side (rank j's columns at j * n) bit for bit, eagerly and replayed from a HIP graph
 with new inputs, with no poll timing out.  Then a ShardedDecode(gather="ipc") step of a real NF4 shard pair against
 the oracle GEMV.  (Two ranks on one device exercise the handles, the flags, the epochs / parities and the graph
-capture; xGMI itself needs the driver's multi-GPU run.)"""
+capture; xGMI itself needs the driver's multi-GPU run.)  A second test pins the fail-stop behaviour: a step whose peer
+never pushes gives up after the bounded wait and writes a NaN row (not the stale slots), check() raises, and every
+later step of that exchange stays NaN without waiting again."""
 import os
 import socket
 
@@ -95,6 +97,74 @@ def _worker(rank, world, port, ret):
         dist.destroy_process_group()
 
 
+def _timeout_worker(rank, world, port, ret):
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "bitsandbytes-sycl_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    try:
+        from python_src_quants.parallel import IpcAllGather
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        n = 64
+        ag = IpcAllGather(n, world, rank, device=dev)
+        res["kind"] = ag.memory_kind
+        y = torch.full((1, n), float(rank + 1), device=dev, dtype=torch.bfloat16)
+        rows = torch.zeros(1, world * n, device=dev, dtype=torch.bfloat16)
+        dist.barrier()
+        ag(y, rows)                                # a healthy step first
+        torch.cuda.synchronize()
+        res["healthy"] = bool(torch.equal(rows.float().view(world, n),
+                                          torch.arange(1, world + 1, device=dev).float().view(world, 1).expand(world, n)))
+        dist.barrier()
+        if rank == 0:                              # rank 1 never pushes this step: bounded wait, then poison
+            t0 = time.perf_counter()
+            ag(y, rows)
+            torch.cuda.synchronize()
+            res["wait_s"] = time.perf_counter() - t0
+            res["nan_row"] = bool(torch.isnan(rows.float()).all())
+            res["timeouts"] = ag.timeouts()
+            try:
+                ag.check()
+                res["raised"] = False
+            except RuntimeError:
+                res["raised"] = True
+            rows.zero_()
+            t0 = time.perf_counter()
+            ag(y, rows)                            # latched: NaN at once, no second wait
+            torch.cuda.synchronize()
+            res["latched_s"] = time.perf_counter() - t0
+            res["latched_nan"] = bool(torch.isnan(rows.float()).all())
+            res["timeouts_after"] = ag.timeouts()
+        dist.barrier()
+        ag.close()
+    except Exception as ex:  # noqa: BLE001
+        res["error"] = repr(ex)
+    finally:
+        ret[rank] = res
+        dist.destroy_process_group()
+
+
+def test_ipc_allgather_timeout_poisons_row():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_timeout_worker, args=(world, port, ret), nprocs=world, join=True)
+    got = dict(ret)
+    for r in range(world):
+        assert "error" not in got[r], got[r]
+        assert got[r]["kind"] == "uncached" and got[r]["healthy"], got[r]
+    r0 = got[0]
+    assert r0["nan_row"] and r0["timeouts"] >= 1 and r0["raised"], r0
+    assert r0["latched_nan"] and r0["timeouts_after"] == r0["timeouts"], r0
+    assert r0["latched_s"] < 0.25 * r0["wait_s"], r0
+
+
 def test_ipc_allgather_two_processes_one_gpu():
     world = 2
     port = _free_port()
@@ -104,5 +174,6 @@ def test_ipc_allgather_two_processes_one_gpu():
     got = dict(ret)
     for r in range(world):
         assert "error" not in got[r], got[r]
+        assert got[r]["kind"] == "uncached", got[r]
         assert got[r]["raw"] and got[r]["timeouts"] == 0, got[r]
         assert got[r]["decode"] and got[r]["decode_timeouts"] == 0, got[r]

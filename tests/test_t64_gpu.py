@@ -90,8 +90,8 @@ def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
     """Write-through partial stores (dwords, staged 16-B lines) equal plain ones bit for bit.  The split-K partials summed by each row tile's last workgroup to finish (agent-scope release / acquire
     hand-off, one ticket per row tile) equal the separate k_skinny_reduce launch bit for bit: same additions in split
     order; whole float4 rows (N % 4 == 0, partial last row tile) and the scalar form (N = 193); more than 8 splits
-    (the batched loads' second round).  Ten launches in a row and a HIP-graph replay: every ticket is back at zero
-    after its launch."""
+    (the batched loads' second round).  Ten launches in a row: every ticket is back at zero after its launch.  A
+    captured launch takes the reduce launch (no ticket set is baked into a graph), so its replays give the same bits."""
     F = _F()
     M, N, K = mnk
     torch.manual_seed(N + K + M)
