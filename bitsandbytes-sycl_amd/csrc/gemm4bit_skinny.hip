@@ -217,13 +217,13 @@ k_gemm_4bit_skinny(int N, int M, int K, const T* __restrict__ A, int lda, const 
 }
 
 // out[t, n] = T(sum_s ws[s][t][n]), splits summed in order (fp32), one RNE cast; 4 outputs per thread.
-// The partials were just written by other XCDs (read back through the MALL), so the loads of up to 8 splits
-// are issued together (indices clamped, unconditional) before any add: one round trip for the usual 4..7
-// splits instead of one per split.  Same additions in the same order as a sequential loop.
-template <typename T>
+// The partials were just written by other XCDs (read back through the MALL), so the loads of up to BATCH splits
+// are issued together (indices clamped, unconditional) before any add: one round trip for the usual 2..8
+// splits instead of one per split.  Same additions in the same order as a sequential loop.  BATCH (2, 4 or 8) is the
+// smallest that covers the split count up to 8 (round 5: with BATCH 8 for 4 splits, half the loads re-read split 3).
+template <typename T, int BATCH = 8>
 __global__ void __launch_bounds__(256)
 k_skinny_reduce(const float* __restrict__ ws, int nsplit, int M, int N, T* __restrict__ out, int ldc) {
-  constexpr int BATCH = 8;
   const long long mn = (long long)M * N;
   const long long i0 = 4 * ((long long)blockIdx.x * 256 + threadIdx.x);
   if (i0 >= mn) return;
@@ -367,11 +367,7 @@ bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uin
   };
   if (nested) dispatch(std::true_type{});
   else dispatch(std::false_type{});
-  if (s > 1) {
-    const long long mn = (long long)m * n;
-    hipLaunchKernelGGL((k_skinny_reduce<T>), dim3((unsigned)((mn / 4 + 255) / 256 + 1)), dim3(256), 0, current_stream(), ws, s,
-                       n, m, out, ldc);
-  }
+  if (s > 1) launch_splitk_rows_reduce<T>(ws, s, n, m, out, ldc);
   return true;
 }
 
@@ -379,8 +375,13 @@ bool launch_gemm_4bit_skinny(int m, int n, int k, const T* A, int lda, const uin
 template <typename T>
 void launch_splitk_rows_reduce(const float* ws, int nsplit, int rows, int cols, T* out, int ldc) {
   const long long mn = (long long)rows * cols;
-  hipLaunchKernelGGL((k_skinny_reduce<T>), dim3((unsigned)((mn / 4 + 255) / 256 + 1)), dim3(256), 0, current_stream(), ws,
-                     nsplit, rows, cols, out, ldc);
+  const dim3 grid((unsigned)((mn / 4 + 255) / 256 + 1));
+  if (nsplit <= 2)
+    hipLaunchKernelGGL((k_skinny_reduce<T, 2>), grid, dim3(256), 0, current_stream(), ws, nsplit, rows, cols, out, ldc);
+  else if (nsplit <= 4)
+    hipLaunchKernelGGL((k_skinny_reduce<T, 4>), grid, dim3(256), 0, current_stream(), ws, nsplit, rows, cols, out, ldc);
+  else
+    hipLaunchKernelGGL((k_skinny_reduce<T, 8>), grid, dim3(256), 0, current_stream(), ws, nsplit, rows, cols, out, ldc);
 }
 template void launch_splitk_rows_reduce<bf16_t>(const float*, int, int, int, bf16_t*, int);
 template void launch_splitk_rows_reduce<fp16_t>(const float*, int, int, int, fp16_t*, int);

@@ -177,6 +177,11 @@ constexpr int HG_V = 16 + 8192;
 // profiles/lab/r04_store_policy.txt)
 constexpr int HG_V_CWT = 32768;
 static int g_hg_cwt = 1;
+// variant bit: the 16-bit full-tile epilogue interleaved per 16-row group -- group i's outputs are converted (the bf16 /
+// fp16 casts, or int8's mm_dequant) and staged while group i - 1's rows are read back and stored, so the VALU of the
+// conversion overlaps the store stream instead of preceding all of it (chgemm_set_epilogue; round 5)
+constexpr int HG_V_EPI = 65536;
+static int g_hg_epi = 1;
 constexpr int HG_V_ALT = 8 + 16 + 4096;
 static int g_hgemm_variant = 0;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
@@ -862,29 +867,22 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
           bsv[j] = bias ? *reinterpret_cast<const uint2*>(bias + nb + 16 * j) : make_uint2(0u, 0u);
       }
     }
-#pragma unroll
-    for (int i = 0; i < WI; ++i) {
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) {
-        uint2 v;
-        if constexpr (OP == HG_BF16 || OP == HG_FP16) {
-          using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
-          v.x = cvt_pk<T>(acc[j][i][0], acc[j][i][1]);
-          v.y = cvt_pk<T>(acc[j][i][2], acc[j][i][3]);
-        } else if constexpr (OP == HG_I8_DEQ) {
-          auto bf = [&](uint32_t w, int hi) { return (float)__builtin_bit_cast(fp16_t, (uint16_t)(w >> (16 * hi))); };
-          v.x = mm_dequant_pair(acc[j][i][0], acc[j][i][1], rsv[i], csv[j][0], csv[j][1], bf(bsv[j].x, 0), bf(bsv[j].x, 1));
-          v.y = mm_dequant_pair(acc[j][i][2], acc[j][i][3], rsv[i], csv[j][2], csv[j][3], bf(bsv[j].y, 0), bf(bsv[j].y, 1));
-        }
-        *reinterpret_cast<uint2*>(ep + (16 * i + (lane_e & 15)) * EPI_PITCH + 2 * (16 * j + 4 * (lane_e >> 4))) = v;
-        __builtin_amdgcn_sched_barrier(0);   // one accumulator at a time: no VGPR burst that displaces AGPRs
+    auto convert = [&](int i, int j) {                   // accumulator (j, i) -> its 8 B of the wave's staging rows
+      uint2 v;
+      if constexpr (OP == HG_BF16 || OP == HG_FP16) {
+        using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
+        v.x = cvt_pk<T>(acc[j][i][0], acc[j][i][1]);
+        v.y = cvt_pk<T>(acc[j][i][2], acc[j][i][3]);
+      } else if constexpr (OP == HG_I8_DEQ) {
+        auto bf = [&](uint32_t w, int hi) { return (float)__builtin_bit_cast(fp16_t, (uint16_t)(w >> (16 * hi))); };
+        v.x = mm_dequant_pair(acc[j][i][0], acc[j][i][1], rsv[i], csv[j][0], csv[j][1], bf(bsv[j].x, 0), bf(bsv[j].x, 1));
+        v.y = mm_dequant_pair(acc[j][i][2], acc[j][i][3], rsv[i], csv[j][2], csv[j][3], bf(bsv[j].y, 0), bf(bsv[j].y, 1));
       }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): the wave reads back only its own region
+      *reinterpret_cast<uint2*>(ep + (16 * i + (lane_e & 15)) * EPI_PITCH + 2 * (16 * j + 4 * (lane_e >> 4))) = v;
+    };
     uint8_t* cbase = reinterpret_cast<uint8_t*>(Cv) + ((long long)(m0 + 16 * WI * wm) * ldc + n0 + 16 * WJ * wn) * 2;
     constexpr int CPR = 2 * WJ, RPI = 64 / CPR;          // 16-B chunks per output row, rows per wave instruction
-#pragma unroll 8
-    for (int it = 0; it < 16 * WI / RPI; ++it) {
+    auto store_rows = [&](int it) {                      // store instruction `it`: rows RPI it .. RPI it + RPI - 1
       const int row = RPI * it + lane_e / CPR, c16 = lane_e % CPR;
       const uint4 v = *reinterpret_cast<const uint4*>(ep + row * EPI_PITCH + 16 * c16);
       uint8_t* dst = cbase + (long long)row * ldc * 2 + 16 * c16;
@@ -892,6 +890,63 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
         asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"((hg_u32x4_t){v.x, v.y, v.z, v.w}) : "memory");
       else
         *reinterpret_cast<uint4*>(dst) = v;
+    };
+    if ((V & HG_V_EPI) != 0 && (long long)ldc * 2 * 16 * WI < 0x7FFFFFFFLL) {
+      // per 16-row group i: convert + stage its WJ accumulators; group i - 1 (staged and drained by lgkmcnt(0) after its
+      // last write) is read back and stored in SPG instructions spread over group i's conversions.  The stores go through a
+      // buffer resource on the wave's output corner: one lane-offset VGPR for all of them, the row step in an SGPR (a
+      // 64-bit address per store made the 256 x 256 bf16 kind spill here)
+      constexpr int SPG = 16 / RPI, EVERY = WJ / SPG;
+      const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, 0x7FFFFFFF, 0x00020000);
+      const uint32_t ldc2 = (uint32_t)ldc * 2u;
+      const uint32_t loff = (uint32_t)(lane_e / CPR) * ldc2 + 16u * (uint32_t)(lane_e % CPR);
+      // store instruction `it` = rows RPI it .. + RPI - 1 of the wave's region; its read-back is issued one slot ahead of
+      // its store, so the store finds the data landed (no LDS round trip exposed per store)
+      auto read_rows = [&](int it) -> hg_u32x4_t {
+        return *reinterpret_cast<const hg_u32x4_t*>(ep + (RPI * it + lane_e / CPR) * EPI_PITCH + 16 * (lane_e % CPR));
+      };
+      auto store_rows_v = [&](const hg_u32x4_t& v, int it) {
+        const int soff = (int)((uint32_t)(RPI * it) * ldc2);
+        if constexpr ((V & HG_V_CWT) != 0)               // device-scope write-through (sc1): no dirty C lines left
+          __builtin_amdgcn_raw_buffer_store_b128(v, cr, (int)loff, soff, 16);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(v, cr, (int)loff, soff, 0);
+      };
+      hg_u32x4_t pv = {0u, 0u, 0u, 0u};
+      int pk = -1;
+      auto slot = [&](int it) {                          // store the pending rows, read `it` (-1: only store)
+        if (pk >= 0) store_rows_v(pv, pk);
+        if (it >= 0) pv = read_rows(it);
+        pk = it;
+      };
+#pragma unroll
+      for (int i = 0; i < WI; ++i) {
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) {
+          convert(i, j);
+          __builtin_amdgcn_sched_barrier(0);             // one accumulator at a time: no VGPR burst that displaces AGPRs
+          if (i > 0 && j % EVERY == EVERY - 1) {
+            slot(SPG * (i - 1) + j / EVERY);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0): group i staged (the wave reads back only its own rows)
+      }
+#pragma unroll
+      for (int s = 0; s < SPG; ++s) slot(SPG * (WI - 1) + s);
+      slot(-1);
+    } else {
+#pragma unroll
+      for (int i = 0; i < WI; ++i) {
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) {
+          convert(i, j);
+          __builtin_amdgcn_sched_barrier(0);             // one accumulator at a time: no VGPR burst that displaces AGPRs
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): the wave reads back only its own region
+#pragma unroll 8
+      for (int it = 0; it < 16 * WI / RPI; ++it) store_rows(it);
     }
   } else if (full) {
     if constexpr (OP == HG_I8_I32) {                   // int32: one 16-B store per accumulator already
@@ -1031,7 +1086,9 @@ static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void
       // one side step every `every` k-tiles of the k-tiles that have a B3 (all but a workgroup's last)
       const int steps = pl.kchunk - 1;
       sd.every = steps > 0 ? std::max(1, (steps + sd.iters - 1) / sd.iters) : 1;
-      hgemm_launch_side<OP, V, WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, sd);
+      // (the side form keeps the round-4 epilogue: with the side's state live the interleaved one spills)
+      hgemm_launch_side<OP, (V & ~HG_V_EPI), WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
+                                                           ws, sd);
       return;
     }
   }
@@ -1053,21 +1110,24 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   if (pl.splits > 1 && (ws == nullptr || ((uintptr_t)ws & 15) ||
                         ws_bytes < (long long)pl.splits * m * n * (long long)sizeof(float)))
     pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, false, full_only);      // no (large enough) workspace: no split
+  // variant bits of the launched kernel: write-through C (g_hg_cwt) and the interleaved epilogue (g_hg_epi, with it)
+  auto by_shape = [&](auto vtag) {
+    constexpr int VV = decltype(vtag)::value;
+    if (pl.wi == 8 && pl.wj == 8)
+      hgemm_launch_shape<OP, VV, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+    else if constexpr (FP) {
+      if (pl.wi == 8) hgemm_launch_shape<OP, VV, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+      else hgemm_launch_shape<OP, VV, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+    }
+  };
   if (g_hgemm_variant == 1) {
     hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
-  } else if (pl.wi == 8 && pl.wj == 8 && g_hg_cwt) {
-    hgemm_launch_shape<OP, HG_V | HG_V_CWT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws,
-                                                  side);
-  } else if (pl.wi == 8 && pl.wj == 8) {
-    hgemm_launch_shape<OP, HG_V, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-  } else if constexpr (FP) {
-    if (g_hg_cwt) {
-      if (pl.wi == 8) hgemm_launch_shape<OP, HG_V | HG_V_CWT, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-      else hgemm_launch_shape<OP, HG_V | HG_V_CWT, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-    } else {
-      if (pl.wi == 8) hgemm_launch_shape<OP, HG_V, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-      else hgemm_launch_shape<OP, HG_V, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-    }
+  } else if (g_hg_cwt && g_hg_epi) {
+    by_shape(std::integral_constant<int, HG_V | HG_V_CWT | HG_V_EPI>{});
+  } else if (g_hg_cwt) {
+    by_shape(std::integral_constant<int, HG_V | HG_V_CWT>{});
+  } else {
+    by_shape(std::integral_constant<int, HG_V>{});
   }
   if constexpr (FP) {
     using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
@@ -1182,6 +1242,13 @@ void chgemm_tn_plan(int m, int n, int k, int* out) {
 int chgemm_set_c_store(int wt) {
   const int prev = bnb::g_hg_cwt;
   bnb::g_hg_cwt = wt ? 1 : 0;
+  return prev;
+}
+// [additive, testing] 1 (default): the interleaved 16-bit epilogue (HG_V_EPI, with write-through C), 0: the round-4 one
+// (convert and stage everything, then store); returns the previous setting
+int chgemm_set_epilogue(int v) {
+  const int prev = bnb::g_hg_epi;
+  bnb::g_hg_epi = v ? 1 : 0;
   return prev;
 }
 int chgemm_set_side_mode(int v) {

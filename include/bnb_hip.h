@@ -272,6 +272,9 @@ int chgemm_set_side_mode(int v);
 int chgemm_set_c_store(int wt);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);
+/* [additive, testing] k_hgemm's 16-bit epilogue: 1 (default) = interleaved per 16-row group (conversion overlapped with
+ * the previous group's stores), 0 = the round-4 form; bit-identical outputs; returns the previous setting */
+int chgemm_set_epilogue(int v);
 /* [additive, testing] the launch plan of chgemm_tn_ws_* for (m, n, k): out = {WI, WJ, splits, k-tiles per split};
  * the output tile is 32 WI x 32 WJ (256 x 256, 256 x 128 or 128 x 256) */
 void chgemm_tn_plan(int m, int n, int k, int* out);

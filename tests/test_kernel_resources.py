@@ -67,9 +67,12 @@ def test_hgemm_tile3_dma_count_between_waits(tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     text = s.read_text()
-    bodies = re.findall(r"^(_ZN3bnb7k_hgemmILi\dELi(?:8208|40976)\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.S | re.M)
-    # (40976 = 8208 | HG_V_CWT: the same loop, C stored write-through -- the launched 256 x 256 kind)
+    bodies = re.findall(r"^(_ZN3bnb7k_hgemmILi\dELi(?:8208|40976|106512)\w+):[^\n]*\n(.*?)^\.Lfunc_end", text,
+                        re.S | re.M)
+    # (40976 = 8208 | HG_V_CWT: the same loop, C stored write-through; 106512 = 40976 | HG_V_EPI: and the interleaved
+    # epilogue -- the launched kinds)
     assert any("ELi40976E" in b[0] for b in bodies), "no write-through-C k_hgemm kernels"
+    assert any("ELi106512E" in b[0] for b in bodies), "no interleaved-epilogue k_hgemm kernels"
     assert bodies, "no three-barrier k_hgemm kernels"
     vmem = re.compile(r"^\s*(global_|buffer_|flat_|scratch_)")
     # per tile shape (WI, WJ): LDS-DMA pieces per k-tile and the vmcnt of barrier B3 (HgPlan3 in hgemm.hip)

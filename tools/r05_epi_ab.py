@@ -1,0 +1,98 @@
+"""Round 5 A/B: k_hgemm's interleaved 16-bit epilogue (chgemm_set_epilogue 1, HG_V_EPI) against the round-4 one (0), on
+the library's own entry points, interleaved rounds in one process: bf16 at the metric shape (4096 x 4096 x 11008) and
+4096^3, int8 igemmlt + fused mm_dequant at the same two shapes.  Outputs of both arms compared bit for bit.  Also the
+33..64-token path (11008 x 4096 NF4 nested at 33 / 64 rows, graph replay over 14 weight copies) as routed.
+Usage: python tools/r05_epi_ab.py [rounds]"""
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "bitsandbytes-sycl_amd")]
+import torch  # noqa: E402
+import python_src_quants.functional as F  # noqa: E402
+
+
+def timed(fn, reps=20):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(1)
+    arms = []
+    for (m, n, k) in [(4096, 4096, 11008), (4096, 4096, 4096)]:
+        X = torch.randn(m, k, device=dev, dtype=torch.bfloat16, generator=g)
+        W = (torch.randn(n, k, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        Y = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+
+        def bf16(X=X, W=W, Y=Y, m=m, n=n, k=k):
+            F.pre_call(dev)
+            assert F.lib.chgemm_tn_bf16(m, n, k, F.get_ptr(X), k, F.get_ptr(W), k, F.get_ptr(Y), n) == 0
+        A8 = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8, generator=g)
+        B8 = torch.randint(-127, 128, (n, k), device=dev, dtype=torch.int8, generator=g)
+        rs = torch.rand(m, device=dev, generator=g) * 2 + 0.5
+        cs = torch.rand(n, device=dev, generator=g) * 2 + 0.5
+        bias = torch.randn(n, device=dev, generator=g).half()
+        O8 = torch.empty(m, n, device=dev, dtype=torch.float16)
+        i8 = lambda A8=A8, B8=B8, rs=rs, cs=cs, bias=bias, O8=O8: F.igemmlt_dequant(A8, B8, rs, cs, bias=bias, out=O8)  # noqa
+        arms.append((f"bf16 {m}x{n}x{k}", bf16, Y))
+        arms.append((f"int8 {m}x{n}x{k}", i8, O8))
+    t_end = time.perf_counter() + 0.5
+    while time.perf_counter() < t_end:
+        arms[0][1]()
+        torch.cuda.synchronize()
+    for name, fn, out in arms:
+        res = []
+        for epi in (0, 1):
+            F.lib.chgemm_set_epilogue(epi)
+            out.zero_()
+            fn()
+            torch.cuda.synchronize()
+            res.append(out.clone())
+        print(f"{name}: epilogue 0 == 1 bitwise: {torch.equal(res[0], res[1])}", flush=True)
+    times = {(name, epi): [] for name, _, _ in arms for epi in (0, 1)}
+    for r in range(rounds):
+        for name, fn, _ in arms:
+            for epi in (0, 1):
+                F.lib.chgemm_set_epilogue(epi)
+                for _ in range(3):
+                    fn()
+                times[(name, epi)].append(timed(fn))
+    F.lib.chgemm_set_epilogue(1)
+    for name, _, _ in arms:
+        a, b = statistics.median(times[(name, 0)]), statistics.median(times[(name, 1)])
+        print(f"{name}: round-4 epilogue {a:7.1f} us   interleaved {b:7.1f} us   ({(b - a) / a * 100:+.1f} %)", flush=True)
+    # the 33..64-token path as routed (t64 + the reduce launch), graph replay over 14 weight copies
+    n_out, k_in = 11008, 4096
+    ws = []
+    for _ in range(14):
+        W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        ws.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True))
+    for mrows in (33, 48, 64):
+        x = torch.randn(mrows, k_in, device=dev, dtype=torch.bfloat16, generator=g)
+        out = torch.empty(mrows, n_out, device=dev, dtype=torch.bfloat16)
+        calls = [(lambda q=q, st=st: F.gemm_4bit(x, q, st, out=out)) for q, st in ws]
+        for c in calls:
+            c()
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for c in calls:
+                c()
+        for _ in range(3):
+            gr.replay()
+        t = min(timed(gr.replay, reps=10) for _ in range(3)) / len(calls)
+        print(f"gemm_4bit 11008x4096 nested, {mrows} rows: {t:6.2f} us per call (graph replay, 14 copies)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
