@@ -104,7 +104,7 @@ __device__ __forceinline__ float t64_load_dev(__amdgpu_buffer_rsrc_t r, uint32_t
 // The split-K combine of one row tile (rows row0 .. row0 + 191, every token), run by the row tile's last workgroup to
 // finish: out[t][row] = T(ws[0][t][row] + ws[1][t][row] + ... ) -- k_skinny_reduce's additions in its order, so the
 // outputs are bit-identical to the two-launch form.
-template <typename T>
+template <typename T, int NT = T64_THREADS>
 __device__ __forceinline__ void t64_combine(__amdgpu_buffer_rsrc_t wsr, int ks, int M, int N, int row0,
                                             T* __restrict__ out, int ldc, int tid) {
   const uint32_t mn = (uint32_t)M * (uint32_t)N;
@@ -112,13 +112,13 @@ __device__ __forceinline__ void t64_combine(__amdgpu_buffer_rsrc_t wsr, int ks, 
   if ((N & 3) == 0) {                                        // row0 % 4 == 0 too: whole float4s
     // element e = tid + 256 j (j < 12 covers 64 tokens x 48 float4s): every load of KB splits x 12 elements in
     // flight before the adds -- one round trip per KB splits instead of one per element
-    constexpr int EPT = (64 * T64_ROWS / 4) / T64_THREADS, KB = 4;
+    constexpr int EPT = (64 * T64_ROWS / 4) / NT, KB = 4;
     const int per_t = rows >> 2, total = M * per_t;
     const bool st8 = (((uintptr_t)out & 7) == 0) && (ldc & 3) == 0;
     uint32_t off[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int e = min(tid + T64_THREADS * j, total - 1), t = e / per_t, c = e - t * per_t;
+      const int e = min(tid + NT * j, total - 1), t = e / per_t, c = e - t * per_t;
       off[j] = (uint32_t)t * (uint32_t)N + (uint32_t)(row0 + 4 * c);
     }
     float4 s[EPT];
@@ -142,7 +142,7 @@ __device__ __forceinline__ void t64_combine(__amdgpu_buffer_rsrc_t wsr, int ks, 
     }
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      const int e = tid + T64_THREADS * j;
+      const int e = tid + NT * j;
       if (e >= total) break;
       const int t = e / per_t, c = e - t * per_t;
       T* dst = out + (long long)t * ldc + row0 + 4 * c;
@@ -154,7 +154,7 @@ __device__ __forceinline__ void t64_combine(__amdgpu_buffer_rsrc_t wsr, int ks, 
       }
     }
   } else {
-    for (int e = tid; e < M * rows; e += T64_THREADS) {
+    for (int e = tid; e < M * rows; e += NT) {
       const int t = e / rows, r = e - t * rows;
       const uint32_t off = (uint32_t)t * (uint32_t)N + (uint32_t)(row0 + r);
       float s = t64_load_dev(wsr, off);
@@ -171,45 +171,56 @@ __device__ __forceinline__ void t64_combine(__amdgpu_buffer_rsrc_t wsr, int ks, 
 // ABL (lab ablations, timing only): 1 = no vmcnt waits, 2 = no token DMA after the prologue, 4 = no weight DMA after
 // the prologue, 8 = no MFMAs, 16 = no table lookups, 32 = no output / partial stores, 64 = no table build, 128 = no
 // barriers in the loop, 256 = no token fragment reads
-template <typename T, bool NESTED, int ABL = 0>
-__global__ void __launch_bounds__(T64_THREADS, 1)
+// KP (round 5): waves per 48-row set.  KP = 1: the round-4 kernel, 4 waves (one per SIMD), each wave both blocks of every
+// 2-block half-group.  KP = 2: 8 waves (two per SIMD), the waves w and w + 4 of a row set take the half-group's first and
+// second block -- the same LDS slots, DMA pieces split between them, half the registers each -- so one wave's VALU (the
+// table lookups, the per-block absmax fmas) and LDS reads run beside the other's MFMAs; the two partial sums of a row
+// set meet in LDS at the end (first + second, fixed order: deterministic).
+template <typename T, bool NESTED, int ABL = 0, int KP = 1>
+__global__ void __launch_bounds__(T64_THREADS * KP, KP)
 k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
                 SkStats st, const float* __restrict__ code, T* __restrict__ out, int ldc, float* __restrict__ ws,
                 int ksplit, int kc, uint32_t* __restrict__ tickets, int pstore) {
-  constexpr int WOPS = (NESTED ? 2 : 1) + T64_WPIECES;       // VMEM instructions of one weight-group issue
-  constexpr int TOPS = T64_TPIECES;                          // ... of one token half-group issue
+  static_assert(KP == 1 || KP == 2, "one or two waves per row set");
+  constexpr int NT = T64_THREADS * KP;                       // threads of the workgroup
+  constexpr int WPW = T64_WPIECES / KP;                      // weight pieces of a group issued by each wave of the set
+  constexpr int WOPS = (NESTED ? 2 : 1) + WPW;               // VMEM instructions of one weight-group issue (per wave)
+  constexpr int TOPS = T64_TPIECES / KP;                     // ... of one token half-group issue
+  constexpr int NB2 = 2 / KP;                                // blocks of a half-group this wave consumes
   __shared__ __attribute__((aligned(16))) uint8_t sm[T64_LDS];
   uint8_t* table = sm;
   auto code2s_at = [&](uint32_t t) -> const float& { return *reinterpret_cast<const float*>(sm + T64_OFF_C2 + 4 * t); };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rs = wave & 3, kp = wave >> 2;                   // row set, k part (KP = 1: rs = wave, kp = 0)
   const int n = lane & 15, g = lane >> 4;
   const int bid = blockIdx.x, rt = bid / ksplit, sp = bid - rt * ksplit;
-  const int r0 = rt * T64_ROWS + wave * 16 * T64_RG;         // this wave's first weight row
+  const int r0 = rt * T64_ROWS + rs * 16 * T64_RG;           // this wave's first weight row
   const int ngr = K >> 8, gr0 = sp * kc, ng = min(kc, ngr - gr0);   // this workgroup's groups (>= 1, host rule)
 
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)sm);
   // token pieces: this wave's pieces q = 4 wave + i of a half-group slot; lane l -> token row t = 4 q + (l >> 4),
   // physical 16-B slot p = l & 15 holding logical slot p ^ (t & 15) (k = 8 x logical slot within the 128 k)
-  uint32_t toff[T64_TPIECES];
+  uint32_t toff[TOPS];
 #pragma unroll
-  for (int i = 0; i < T64_TPIECES; ++i) {
-    const int q = 4 * wave + i, t = 4 * q + (lane >> 4), p = lane & 15;
+  for (int i = 0; i < TOPS; ++i) {
+    const int q = TOPS * wave + i, t = 4 * q + (lane >> 4), p = lane & 15;
     toff[i] = (uint32_t)min(t, M - 1) * (uint32_t)lda * 2u + 16u * (uint32_t)(p ^ (t & 15));
   }
   // weight pieces: piece j = rows 8 j .. 8 j + 7 of the wave's 48; lane l -> row 8 j + (l >> 3), LDS slot l & 7 holding
   // source slot (l & 7) ^ ((row >> 1) & 7)
-  uint32_t woff[T64_WPIECES];
+  // (KP = 2: the pieces 3 kp .. 3 kp + 2 of the set's 6)
+  uint32_t woff[WPW];
 #pragma unroll
-  for (int j = 0; j < T64_WPIECES; ++j) {
-    const int rr = 8 * j + (lane >> 3);
-    woff[j] = (uint32_t)min(r0 + rr, N - 1) * (uint32_t)ldb + 16u * (uint32_t)((lane & 7) ^ ((rr >> 1) & 7));
+  for (int jj = 0; jj < WPW; ++jj) {
+    const int j = WPW * kp + jj, rr = 8 * j + (lane >> 3);
+    woff[jj] = (uint32_t)min(r0 + rr, N - 1) * (uint32_t)ldb + 16u * (uint32_t)((lane & 7) ^ ((rr >> 1) & 7));
   }
   // statistics: lane l -> the wave's row min(l, 47); its first block index (bs = 64: 2 ldb row / 64)
   const uint32_t sblk0 = (uint32_t)((2LL * ldb * min(r0 + min(lane, 16 * T64_RG - 1), N - 1)) >> 6);
   const uint32_t tok_lds = lds0 + T64_OFF_TOK;
-  const uint32_t w_lds = lds0 + T64_OFF_W + wave * 2 * T64_WGRP;
-  const uint32_t s_lds = lds0 + T64_OFF_S + wave * 2 * T64_STAT;
+  const uint32_t w_lds = lds0 + T64_OFF_W + rs * 2 * T64_WGRP;
+  const uint32_t s_lds = lds0 + T64_OFF_S + rs * 2 * T64_STAT;
 
   auto issue_w = [&](int gi, int slot) {                     // weight group gi (clamped) -> this wave's slot
     if constexpr ((ABL & 4) != 0) if (gi >= 2) return;
@@ -221,16 +232,18 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
     } else {
       t64_dma<16>(st.absmax, 4u * j0, s_lds + slot * T64_STAT);
     }
+    // (both waves of a row set load its statistics: the same words into the same slot, so every wave's VMEM count per
+    // group is the same constant)
     const uint8_t* src = B + 128LL * G;
 #pragma unroll
-    for (int j = 0; j < T64_WPIECES; ++j) t64_dma_nt<16>(src, woff[j], w_lds + slot * T64_WGRP + 1024 * j);
+    for (int jj = 0; jj < WPW; ++jj) t64_dma_nt<16>(src, woff[jj], w_lds + slot * T64_WGRP + 1024 * (WPW * kp + jj));
   };
   auto issue_t = [&](int hi, int slot) {                     // token half-group hi (clamped) -> token slot
     if constexpr ((ABL & 2) != 0) if (hi >= 2) return;
     const int h = min(hi, 2 * ng - 1);
     const T* src = A + 64LL * (4 * gr0 + 2 * h);             // k0 = 64 x (first block of the half-group)
 #pragma unroll
-    for (int i = 0; i < T64_TPIECES; ++i) t64_dma<16>(src, toff[i], tok_lds + slot * T64_TOK + 1024 * (4 * wave + i));
+    for (int i = 0; i < TOPS; ++i) t64_dma<16>(src, toff[i], tok_lds + slot * T64_TOK + 1024 * (TOPS * wave + i));
   };
 
   f32x4_t acc[T64_RG][4];
@@ -246,19 +259,21 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
     // One wave per SIMD: nothing else hides an LDS round trip, so every read of the half-group is issued before any
     // is used -- token fragments of both blocks, the weight words and statistics of all row groups, then all table
     // lookups -- and only then the 48 MFMAs (one basic block; hipcc waits on lgkmcnt just before each first use).
+    // (KP = 2: only block kp of the half-group -- b2 below runs over this wave's NB2 blocks, bk = its block index)
     const int ws_slot = gi & 1;
     const uint8_t* tk = sm + T64_OFF_TOK + half * T64_TOK;
-    const uint8_t* wr = sm + T64_OFF_W + (wave * 2 + ws_slot) * T64_WGRP;
-    const uint8_t* sr = sm + T64_OFF_S + (wave * 2 + ws_slot) * T64_STAT;
-    uint2 wv[2][T64_RG];
+    const uint8_t* wr = sm + T64_OFF_W + (rs * 2 + ws_slot) * T64_WGRP;
+    const uint8_t* sr = sm + T64_OFF_S + (rs * 2 + ws_slot) * T64_STAT;
+    auto bk = [&](int b2) { return KP == 2 ? kp : b2; };
+    uint2 wv[NB2][T64_RG];
     uint32_t q4[T64_RG];
-    float a2[T64_RG], a[2][T64_RG];
+    float a2[T64_RG], a[NB2][T64_RG];
 #pragma unroll
     for (int rg = 0; rg < T64_RG; ++rg) {
       const int rr = 16 * rg + n;
 #pragma unroll
-      for (int b2 = 0; b2 < 2; ++b2) {
-        const int slot16 = (2 * (2 * half + b2) + (g >> 1)) ^ ((rr >> 1) & 7);
+      for (int b2 = 0; b2 < NB2; ++b2) {
+        const int slot16 = (2 * (2 * half + bk(b2)) + (g >> 1)) ^ ((rr >> 1) & 7);
         wv[b2][rg] = *reinterpret_cast<const uint2*>(wr + rr * 128 + 16 * slot16 + 8 * (g & 1));
       }
       if constexpr (NESTED) {
@@ -266,17 +281,17 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
         a2[rg] = *reinterpret_cast<const float*>(sr + 256 + 4 * rr);
       } else {
 #pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2) a[b2][rg] = *reinterpret_cast<const float*>(sr + 16 * rr + 4 * (2 * half + b2));
+        for (int b2 = 0; b2 < NB2; ++b2) a[b2][rg] = *reinterpret_cast<const float*>(sr + 16 * rr + 4 * (2 * half + bk(b2)));
       }
     }
-    uint4 xf[2][4][2];                                       // tokens: A tile mt, lane (t = n, g): row 16 mt + n
+    uint4 xf[NB2][4][2];                                     // tokens: A tile mt, lane (t = n, g): row 16 mt + n
 #pragma unroll
-    for (int b2 = 0; b2 < 2; ++b2)
+    for (int b2 = 0; b2 < NB2; ++b2)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const int ls = 8 * b2 + 2 * g + s;                 // logical 16-B slot: k 64 b2 + 16 g + 8 s
+          const int ls = 8 * bk(b2) + 2 * g + s;             // logical 16-B slot: k 64 b2 + 16 g + 8 s
           if constexpr ((ABL & 256) != 0) xf[b2][mt][s] = make_uint4(ls, mt, n, 0);
           else xf[b2][mt][s] = *reinterpret_cast<const uint4*>(tk + (16 * mt + n) * 256 + 16 * (ls ^ n));
         }
@@ -285,12 +300,12 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
 #pragma unroll
       for (int rg = 0; rg < T64_RG; ++rg)
 #pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2)
-          a[b2][rg] = __fadd_rn(__fmul_rn(code2s_at((q4[rg] >> (8 * (2 * half + b2))) & 0xFF), a2[rg]), offset);
+        for (int b2 = 0; b2 < NB2; ++b2)
+          a[b2][rg] = __fadd_rn(__fmul_rn(code2s_at((q4[rg] >> (8 * (2 * half + bk(b2)))) & 0xFF), a2[rg]), offset);
     }
-    uint4 bf[2][T64_RG][2];                                  // weight operands: byte i of the word -> entry, lane copy
+    uint4 bf[NB2][T64_RG][2];                                // weight operands: byte i of the word -> entry, lane copy
 #pragma unroll
-    for (int b2 = 0; b2 < 2; ++b2)
+    for (int b2 = 0; b2 < NB2; ++b2)
 #pragma unroll
       for (int rg = 0; rg < T64_RG; ++rg)
 #pragma unroll
@@ -305,7 +320,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
           bf[b2][rg][s] = make_uint4(l[0], l[1], l[2], l[3]);
         }
 #pragma unroll
-    for (int b2 = 0; b2 < 2; ++b2)
+    for (int b2 = 0; b2 < NB2; ++b2)
 #pragma unroll
       for (int rg = 0; rg < T64_RG; ++rg) {
         f32x4_t blk[4];
@@ -332,7 +347,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   if constexpr (NESTED) {
     // (the offset too: a plain load of it would be a VMEM load hipcc waits for with vmcnt(0) -- inside the loop, where
     // it drained every in-flight piece each group)
-    t64_dma<4>(st.code2, 4u * (uint32_t)(64 * wave + lane), lds0 + T64_OFF_C2 + 256 * wave);
+    if (wave < 4) t64_dma<4>(st.code2, 4u * (uint32_t)(64 * wave + lane), lds0 + T64_OFF_C2 + 256 * wave);
     if (wave == 0) t64_dma<4>(st.offset, 0u, lds0 + T64_OFF_OFS);
   }
   issue_w(0, 0);
@@ -348,12 +363,16 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
     float hi = dt[0], lo = dt[0];
 #pragma unroll
     for (int j = 1; j < 16; ++j) {
-      hi = (tid >> 4) == j ? dt[j] : hi;
+      hi = ((tid & 255) >> 4) == j ? dt[j] : hi;
       lo = (tid & 15) == j ? dt[j] : lo;
     }
     const uint32_t v = Dot2<T>::pair(hi, lo);
+    // (KP = 2: threads 256.. write the same entries' other halves: entry tid & 255, copies 4 (tid >> 8) .. + 3)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * tid + 16 * ((k + tid) & 7)) = make_uint4(v, v, v, v);
+    for (int k = 0; k < 8 / KP; ++k) {
+      const int e = tid & 255, kk = k + (8 / KP) * (tid >> 8);
+      *reinterpret_cast<uint4*>(table + 256 * e + 16 * ((kk + e) & 7)) = make_uint4(v, v, v, v);
+    }
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);                      // lgkmcnt(0): the table is written (barrier at the wait)
 
@@ -380,6 +399,31 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   }
   wait_vmcnt0();                                                           // no LDS-DMA may outlive the workgroup
 
+  // ---- KP = 2: the second wave of each row set hands its partial sums to the first through LDS (the table region, free
+  // once every wave is past its last lookup); the first adds them (first + second) and does the stores below
+  if constexpr (KP == 2) {
+    float* pb = reinterpret_cast<float*>(sm);                // 4 sets x 48 rows x 64 tokens x 4 B = 48 KiB
+    __syncthreads();
+    if (kp == 1) {
+#pragma unroll
+      for (int rg = 0; rg < T64_RG; ++rg)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pb[(((rs * T64_RG + rg) * 4 + mt) * 4 + i) * 64 + lane] = acc[rg][mt][i];
+    }
+    __syncthreads();
+    if (kp == 0) {
+#pragma unroll
+      for (int rg = 0; rg < T64_RG; ++rg)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[rg][mt][i] = acc[rg][mt][i] + pb[(((rs * T64_RG + rg) * 4 + mt) * 4 + i) * 64 + lane];
+    }
+  }
+  const bool storer = KP == 1 || kp == 0;                   // (wave-uniform) the waves that hold the summed tile
+
   // ---- outputs: acc[rg][mt][i] = token 16 mt + 4 g + i, weight row r0 + 16 rg + n (ABL 32: stored only where the
   // value is an impossible one -- the computation stays live, the stores go).  A whole tile (64 tokens, 192 rows in
   // range) stores unpredicated from a wave-uniform base per (token tile, i) plus one 32-bit lane offset; edge tiles
@@ -396,21 +440,24 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
       // 196 floats: the 4 token rows of one write are 2-way on the banks) then 16-B stores, each wave's 1 KiB contiguous
       float* stage = reinterpret_cast<float*>(sm);             // the table: every wave is past its last lookup
       __syncthreads();
-      const int wr0 = wave * 16 * T64_RG;
+      const int wr0 = rs * 16 * T64_RG;
+      if (storer) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int rg = 0; rg < T64_RG; ++rg) stage[(16 * mt + 4 * g + i) * T64_STAGE_LD + wr0 + 16 * rg + n] = acc[rg][mt][i];
+            for (int rg = 0; rg < T64_RG; ++rg) stage[(16 * mt + 4 * g + i) * T64_STAGE_LD + wr0 + 16 * rg + n] = acc[rg][mt][i];
+      }
       __syncthreads();
       const uint32_t b0 = (uint32_t)sp * 64u * (uint32_t)N + (uint32_t)(rt * T64_ROWS);
 #pragma unroll
-      for (int j = 0; j < (64 * T64_ROWS / 4) / T64_THREADS; ++j) {
-        const int e = tid + T64_THREADS * j, t = e / (T64_ROWS / 4), c = e - t * (T64_ROWS / 4);
+      for (int j = 0; j < (64 * T64_ROWS / 4) / NT; ++j) {
+        const int e = tid + NT * j, t = e / (T64_ROWS / 4), c = e - t * (T64_ROWS / 4);
         const float4 v = *reinterpret_cast<const float4*>(stage + t * T64_STAGE_LD + 4 * c);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hg_u32x4, v), wsr, (int)(4u * (b0 + (uint32_t)t * (uint32_t)N + 4u * c)), 0, 16);
       }
+    } else if (!storer) {
     } else if (ksplit > 1 && wt != 0) {
       const uint32_t b0 = (uint32_t)sp * 64u * (uint32_t)N + loff;
 #pragma unroll
@@ -441,7 +488,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
           for (int rg = 0; rg < T64_RG; ++rg) p[loo + 16 * rg] = Io<T>::from_f32(acc[rg][mt][i]);
         }
     }
-  } else {
+  } else if (storer) {
 #pragma unroll
     for (int rg = 0; rg < T64_RG; ++rg) {
       const int row = r0 + 16 * rg + n;
@@ -479,7 +526,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
     __syncthreads();
     if (last[0] == 0u) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    t64_combine<T>(wsr, ksplit, M, N, rt * T64_ROWS, out, ldc, tid);
+    t64_combine<T, NT>(wsr, ksplit, M, N, rt * T64_ROWS, out, ldc, tid);
     if (tid == 0) __hip_atomic_store(&tickets[rt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -501,6 +548,8 @@ int g_t64_combine = 0;
 // boundary then has no dirty partials to write back (11008 x 4096 at 64 rows 22.9 -> 21.8 us, 4096 x 11008 24.7 ->
 // 22.3, 4096^2 19.0 -> 15.5; write-through dwords within 0.2 us of the lines; profiles/lab/r04_t64.txt)
 int g_t64_pstore = 2;
+// waves per 48-row set (cgemm_4bit_set_t64_waves): 1 = the round-4 4-wave kernel, 2 = 8 waves, two per SIMD (round 5)
+int g_t64_kp = 1;
 
 // this launch's ticket set on the current device (nullptr: use the reduce launch).  Never during HIP-graph capture: a
 // captured launch would bake one ticket set into the graph, and its replays could then share counters with eager
@@ -592,6 +641,13 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
       case 30 + 32 + 64 + 128 + 256: lab(k_gemm_4bit_t64<T, true, 30 + 32 + 64 + 128 + 256>); break;
       default: lab(k_gemm_4bit_t64<T, true>); break;
     }
+  } else if (g_t64_kp == 2) {
+    if (nested)
+      hipLaunchKernelGGL((k_gemm_4bit_t64<T, true, 0, 2>), grid, dim3(2 * T64_THREADS), 0, current_stream(), m, n, k, A,
+                         lda, B, ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
+    else
+      hipLaunchKernelGGL((k_gemm_4bit_t64<T, false, 0, 2>), grid, dim3(2 * T64_THREADS), 0, current_stream(), m, n, k, A,
+                         lda, B, ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
   } else if (nested)
     hipLaunchKernelGGL((k_gemm_4bit_t64<T, true>), grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb,
                        st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
@@ -625,6 +681,13 @@ int cgemm_4bit_set_t64_splits(int ks) {                   // [lab] force the spl
 int cgemm_4bit_set_t64_pstore(int p) {
   const int prev = bnb::g_t64_pstore;
   bnb::g_t64_pstore = p;
+  return prev;
+}
+// [additive, testing] waves per 48-row set of the 33..64-token kernel: 1 = 4 waves (one per SIMD), 2 = 8 waves (two per
+// SIMD; round 5); returns the previous setting
+int cgemm_4bit_set_t64_waves(int kp) {
+  const int prev = bnb::g_t64_kp;
+  bnb::g_t64_kp = kp == 2 ? 2 : 1;
   return prev;
 }
 int cgemm_4bit_set_t64_combine(int on) {

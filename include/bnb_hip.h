@@ -259,6 +259,9 @@ int cgemm_4bit_set_t64_combine(int on);
 /* [additive, testing] that kernel's split-K partial stores: 0 = write-back, 1 = write-through dwords, 2 (default) =
  * write-through 16-B lines staged through LDS; returns the previous setting */
 int cgemm_4bit_set_t64_pstore(int p);
+/* [additive, testing] that kernel's waves per 48-row set: 1 = 4 waves (one per SIMD), 2 = 8 waves (two per SIMD, the
+ * set's blocks alternated between them, partial sums added in LDS); returns the previous setting */
+int cgemm_4bit_set_t64_waves(int kp);
 /* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
  * grid_cap = at most that many workgroups (0 = none); returns the previous p */
 int cdequantize_set_stream_cfg(int p, int grid_cap);

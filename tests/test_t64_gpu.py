@@ -2,7 +2,9 @@
 reduce, every operand by LDS-DMA.  Its arithmetic is the whole-K few-token kernel's (T(code) x tokens summed per
 64-element block on the MFMA, then x absmax), so the bar is the GEMV's / the tile kernels' against the fp64 oracle;
 deterministic; the in-kernel nested decode equals passing the decoded absmax.  Auto at 33..64 rows; forced
-(cgemm_4bit_set_t64_mode(2)) also at 1..32 rows; shapes it does not take (blocksize != 64, K % 256) fall back."""
+(cgemm_4bit_set_t64_mode(2)) also at 1..32 rows; shapes it does not take (blocksize != 64, K % 256) fall back.  Both
+forms of the kernel: 4 waves (one per SIMD) and 8 waves (two per SIMD, the two waves of a row set on alternate blocks,
+their partial sums added in LDS; cgemm_4bit_set_t64_waves)."""
 import ctypes as ct
 
 import numpy as np
@@ -31,7 +33,8 @@ def _close(got, exp, rtol, atol_rel):
 @pytest.mark.parametrize("mnk,mode", [((33, 11008, 4096), 0), ((64, 11008, 4096), 0), ((48, 4096, 11008), 0),
                                       ((64, 4096, 4096), 0), ((40, 1000, 2304), 0), ((64, 193, 256), 0),
                                       ((57, 3584, 8192), 0), ((1, 4096, 4096), 2), ((17, 520, 768), 2)])
-def test_t64_vs_oracle(dev, dtype, nested, qt, bs, mnk, mode):
+@pytest.mark.parametrize("waves", [1, 2])
+def test_t64_vs_oracle(dev, dtype, nested, qt, bs, mnk, mode, waves):
     F = _F()
     M, N, K = mnk
     torch.manual_seed(M * 7 + N + K + bs)
@@ -39,6 +42,7 @@ def test_t64_vs_oracle(dev, dtype, nested, qt, bs, mnk, mode):
     X = torch.randn(M, K, device=dev, dtype=dtype)
     q, st = F.quantize_4bit(W, blocksize=bs, quant_type=qt, compress_statistics=nested)
     prev = F.lib.cgemm_4bit_set_t64_mode(ct.c_int(mode))
+    prev_w = F.lib.cgemm_4bit_set_t64_waves(ct.c_int(waves))
     saved = F.GEMM_4BIT_GEMV_TOKENS
     F.GEMM_4BIT_GEMV_TOKENS = 1
     F.set_fewtok_mode(1)                               # (forced rows <= 32: not the whole-K kernel)
@@ -48,6 +52,7 @@ def test_t64_vs_oracle(dev, dtype, nested, qt, bs, mnk, mode):
         Yp = F.gemm_4bit(X, q, st, absmax=F._absmax_fp32(st))
     finally:
         F.lib.cgemm_4bit_set_t64_mode(ct.c_int(prev))
+        F.lib.cgemm_4bit_set_t64_waves(ct.c_int(prev_w))
         F.set_fewtok_mode(0)
         F.GEMM_4BIT_GEMV_TOKENS = saved
     assert Y.shape == (M, N) and Y.dtype == dtype
@@ -86,7 +91,8 @@ def test_t64_is_the_default_at_33_to_64_rows(dev):
 @pytest.mark.parametrize("mnk", [(64, 11008, 4096), (33, 4096, 11008), (40, 1000, 2304), (64, 193, 4096),
                                  (57, 3584, 8192), (48, 520, 4096)])
 @pytest.mark.parametrize("splits", [0, 3, 11])
-def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
+@pytest.mark.parametrize("waves", [1, 2])
+def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits, waves):
     """Write-through partial stores (dwords, staged 16-B lines) equal plain ones bit for bit.  The split-K partials summed by each row tile's last workgroup to finish (agent-scope release / acquire
     hand-off, one ticket per row tile) equal the separate k_skinny_reduce launch bit for bit: same additions in split
     order; whole float4 rows (N % 4 == 0, partial last row tile) and the scalar form (N = 193); more than 8 splits
@@ -100,6 +106,7 @@ def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
     q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
     prev_ks = F.lib.cgemm_4bit_set_t64_splits(ct.c_int(splits))
     prev_mode = F.lib.cgemm_4bit_set_t64_mode(ct.c_int(2))
+    prev_w = F.lib.cgemm_4bit_set_t64_waves(ct.c_int(waves))
     prev_ps = F.lib.cgemm_4bit_set_t64_pstore(ct.c_int(0))
     try:
         F.lib.cgemm_4bit_set_t64_combine(ct.c_int(0))
@@ -131,5 +138,42 @@ def test_t64_in_kernel_combine_matches_reduce_launch(dev, dtype, mnk, splits):
         F.lib.cgemm_4bit_set_t64_pstore(ct.c_int(prev_ps))
         F.lib.cgemm_4bit_set_t64_mode(ct.c_int(prev_mode))
         F.lib.cgemm_4bit_set_t64_splits(ct.c_int(prev_ks))
+        F.lib.cgemm_4bit_set_t64_waves(ct.c_int(prev_w))
     for o in outs + replays:
         assert torch.equal(o, ref_out)
+
+
+@pytest.mark.parametrize("nested", [False, True])
+def test_t64_eight_waves_close_to_four(dev, nested):
+    """The 8-wave form sums each row set's blocks in two interleaved halves (then first + second): within the GEMM
+    tolerance of the 4-wave form, deterministic, and the same under a HIP-graph replay."""
+    F = _F()
+    N, K, M = 11008, 4096, 64
+    torch.manual_seed(5 + nested)
+    W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    q, st = F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=nested)
+    prev = F.lib.cgemm_4bit_set_t64_waves(ct.c_int(1))
+    try:
+        Y4 = F.gemm_4bit(X, q, st)
+        F.lib.cgemm_4bit_set_t64_waves(ct.c_int(2))
+        Y8 = F.gemm_4bit(X, q, st)
+        Y8b = F.gemm_4bit(X, q, st)
+        out = torch.empty_like(Y8)
+        F.gemm_4bit(X, q, st, out=out)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                F.gemm_4bit(X, q, st, out=out)
+        torch.cuda.current_stream().wait_stream(s)
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        F.lib.cgemm_4bit_set_t64_waves(ct.c_int(prev))
+    assert torch.equal(Y8, Y8b) and torch.equal(out, Y8)
+    e = Y4.float()
+    rms = e.pow(2).mean().sqrt()
+    assert bool(((Y8.float() - e).abs() <= 1e-2 * rms + 1e-2 * e.abs()).all())

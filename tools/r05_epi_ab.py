@@ -77,21 +77,33 @@ def main():
     for _ in range(14):
         W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
         ws.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True))
+    import ctypes as ct
     for mrows in (33, 48, 64):
         x = torch.randn(mrows, k_in, device=dev, dtype=torch.bfloat16, generator=g)
         out = torch.empty(mrows, n_out, device=dev, dtype=torch.bfloat16)
         calls = [(lambda q=q, st=st: F.gemm_4bit(x, q, st, out=out)) for q, st in ws]
-        for c in calls:
-            c()
-        torch.cuda.synchronize()
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr):
+        graphs, res = {}, {}
+        for waves in (1, 2):                      # t64: 4 waves (one per SIMD) / 8 waves (two per SIMD)
+            F.lib.cgemm_4bit_set_t64_waves(ct.c_int(waves))
             for c in calls:
                 c()
-        for _ in range(3):
-            gr.replay()
-        t = min(timed(gr.replay, reps=10) for _ in range(3)) / len(calls)
-        print(f"gemm_4bit 11008x4096 nested, {mrows} rows: {t:6.2f} us per call (graph replay, 14 copies)", flush=True)
+            torch.cuda.synchronize()
+            res[waves] = out.clone()
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for c in calls:
+                    c()
+            graphs[waves] = gr
+        F.lib.cgemm_4bit_set_t64_waves(ct.c_int(1))
+        e = res[1].float()
+        ok = bool(((res[2].float() - e).abs() <= 1e-2 * e.pow(2).mean().sqrt() + 1e-2 * e.abs()).all())
+        ts = {1: [], 2: []}
+        for _ in range(5):
+            for waves in (1, 2):
+                graphs[waves].replay()
+                ts[waves].append(timed(graphs[waves].replay, reps=10) / len(calls))
+        print(f"gemm_4bit 11008x4096 nested, {mrows} rows (graph replay, 14 copies): t64 4 waves "
+              f"{statistics.median(ts[1]):6.2f} us   8 waves {statistics.median(ts[2]):6.2f} us   (close: {ok})", flush=True)
 
 
 if __name__ == "__main__":
