@@ -261,10 +261,17 @@ struct NestedStats {
 // STP: store policy of the 16-B output stores -- 0 default (write-back L2), 1 non-temporal (nt), 2 device-scope
 // write-through (sc1, through a buffer resource: the output below 2 GiB)
 typedef uint32_t dq_u32x4 __attribute__((ext_vector_type(4)));
-template <typename T, int DT, int P, bool NESTED = false, int STP = 0>
+// SQ (round 5; NESTED, P = 8, blocksize 64, blocksize2 >= 64): a wave's pass covers 512 packed dwords = 64 statistics
+// blocks, whose 64 codes are one aligned 64-B run and whose second-level scale is ONE value -- they come by two scalar
+// loads per wave (s_load_dwordx16 + s_load_dword) instead of 8 + 8 per-lane vector loads (lanes 8 i .. 8 i + 7 share a
+// block), leaving the vector-memory pipe the packed loads and the stores only.  Same values, same fp32 operations.
+typedef const __attribute__((address_space(4))) uint32_t* dq_cu32_p;
+typedef const __attribute__((address_space(4))) float* dq_cf32_p;
+template <typename T, int DT, int P, bool NESTED = false, int STP = 0, bool SQ = false>
 __global__ void __launch_bounds__(256)
 k_dequantize_4bit_stream(const uint8_t* __restrict__ A, const float* __restrict__ absmax, T* __restrict__ out,
                          int bs_shift, long long ndw, NestedStats ns = {}) {
+  static_assert(!SQ || (NESTED && P == 8), "scalar statistics: nested, 8 dwords per lane");
   __shared__ float2 s_pair[256];
   __shared__ float s_code2[NESTED ? 256 : 1];
   s_pair[threadIdx.x] = make_float2(code4_value<DT>(threadIdx.x >> 4), code4_value<DT>(threadIdx.x & 15));
@@ -274,20 +281,39 @@ k_dequantize_4bit_stream(const uint8_t* __restrict__ A, const float* __restrict_
     off = *ns.offset;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t* Aw = reinterpret_cast<const uint32_t*>(A);
+  const long long nblk = (ndw + 7) >> 3;                    // (SQ: blocksize 64 = 8 packed dwords per block)
   for (long long base = (long long)blockIdx.x * 256 * P; base < ndw; base += (long long)gridDim.x * 256 * P) {
     uint32_t w[P];
     float am[P];
+    const long long blk0 = (base + 64LL * P * wave) >> 3;   // SQ: the wave's first block (wave-uniform, % 64 == 0)
+    if (SQ && blk0 + 64 <= nblk) {
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-      const long long d = min(base + 64LL * (P * wave + j) + lane, ndw - 1);
-      w[j] = __builtin_nontemporal_load(Aw + d);
-      if constexpr (NESTED) {
-        const long long blk = (8 * d) >> bs_shift;
-        am[j] = __fadd_rn(__fmul_rn(s_code2[ns.q8[blk]], ns.absmax2[blk >> ns.bs2_shift]), off);
-      } else {
-        am[j] = absmax[(8 * d) >> bs_shift];
+      for (int j = 0; j < P; ++j) w[j] = __builtin_nontemporal_load(Aw + min(base + 64LL * (P * wave + j) + lane, ndw - 1));
+      uint32_t qv[16];
+      const dq_cu32_p qc = (dq_cu32_p)(ns.q8 + blk0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) qv[i] = qc[i];
+      const float a2 = *(dq_cf32_p)(ns.absmax2 + (blk0 >> ns.bs2_shift));
+      // dword j of the lane is in block blk0 + 8 j + (lane >> 3): code byte (lane >> 3) & 3 of qv[2 j + (lane >> 5)]
+      const int sh = 8 * ((lane >> 3) & 3);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const uint32_t qw = (lane & 32) ? qv[2 * j + 1] : qv[2 * j];
+        am[j] = __fadd_rn(__fmul_rn(s_code2[(qw >> sh) & 0xFF], a2), off);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const long long d = min(base + 64LL * (P * wave + j) + lane, ndw - 1);
+        w[j] = __builtin_nontemporal_load(Aw + d);
+        if constexpr (NESTED) {
+          const long long blk = (8 * d) >> bs_shift;
+          am[j] = __fadd_rn(__fmul_rn(s_code2[ns.q8[blk]], ns.absmax2[blk >> ns.bs2_shift]), off);
+        } else {
+          am[j] = absmax[(8 * d) >> bs_shift];
+        }
       }
     }
 #pragma unroll
@@ -412,6 +438,8 @@ void quantize_blockwise(const float* code, const T* A, float* absmax, uint8_t* o
 // metric step 263.3 -> 260.2 us, C1 8.85 -> 8.6 us; non-temporal stores 20.8 us alone but a slower step (266.0)
 // (tools/dequant_store_ab.py, tools/bench_knobs.py; profiles/lab/r04_store_policy.txt)
 static int g_dq_p = 8, g_dq_grid_cap = 0, g_dq_store = 2;
+// scalar-loaded nested statistics (SQ above; cdequantize_set_nested_scalar): 1 = where they apply, 0 = off
+static int g_dq_sq = 1;
 template <typename T, int DT, bool NESTED>
 static void launch_dq_stream(const uint8_t* A, const float* absmax, T* out, int bs_shift, long long ndw,
                              const NestedStats& ns) {
@@ -424,6 +452,12 @@ static void launch_dq_stream(const uint8_t* A, const float* absmax, T* out, int 
       hipLaunchKernelGGL(kern, dim3((int)wgs), dim3(256), 0, current_stream(), A, absmax, out, bs_shift, ndw, ns);
     };
     if constexpr (P == 8 && sizeof(T) == 2) {               // store-policy variants (the default shape only)
+      if constexpr (NESTED) {
+        // (64-B aligned codes: each wave's 64-code run is one aligned scalar load; every run read lies inside the codes)
+        if (g_dq_sq && g_dq_store == 2 && ndw * 16 <= 0x7FFFFFFFLL && bs_shift == 6 && ns.bs2_shift >= 6 &&
+            ((uintptr_t)ns.q8 & 63) == 0 && ((uintptr_t)ns.absmax2 & 3) == 0)
+          return launch(k_dequantize_4bit_stream<T, DT, P, NESTED, 2, true>);
+      }
       if (g_dq_store == 1) return launch(k_dequantize_4bit_stream<T, DT, P, NESTED, 1>);
       if (g_dq_store == 2 && ndw * 16 <= 0x7FFFFFFFLL) return launch(k_dequantize_4bit_stream<T, DT, P, NESTED, 2>);
     }
@@ -512,6 +546,13 @@ int cdequantize_set_stream_cfg(int p, int grid_cap) {
   const int prev = g_dq_p;
   g_dq_p = p;
   g_dq_grid_cap = grid_cap;
+  return prev;
+}
+// [additive, testing] nested statistics of k_dequantize_4bit_stream by scalar loads (1, default, where they apply) or per
+// lane (0); bit-identical; returns the previous setting
+int cdequantize_set_nested_scalar(int on) {
+  const int prev = g_dq_sq;
+  g_dq_sq = on ? 1 : 0;
   return prev;
 }
 // [additive, testing] store policy of k_dequantize_4bit_stream's 16-bit outputs (default launch shape): 0 = write-back,

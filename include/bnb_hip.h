@@ -268,6 +268,10 @@ int cdequantize_set_stream_cfg(int p, int grid_cap);
 /* [additive, testing] store policy of that kernel's bf16/fp16 outputs: 0 = write-back, 1 = non-temporal,
  * 2 (default) = device-scope write-through; returns the previous setting */
 int cdequantize_set_store_policy(int policy);
+/* [additive, testing] the nested-statistics dequantise reads each wave's 64 statistic codes and second-level scale by
+ * scalar loads (1, default, where blocksize 64 / blocksize2 >= 64 / 64-B aligned codes allow) or per lane (0);
+ * bit-identical; returns the previous setting */
+int cdequantize_set_nested_scalar(int on);
 /* [additive, testing] k_hgemm side-dequantise A/B bits (chgemm_tn_pf_*); returns the previous value */
 int chgemm_set_side_mode(int v);
 /* [additive, testing] 1 (default): k_hgemm stores C and its split-K partials write-through (device scope), 0:
