@@ -71,13 +71,49 @@ def main():
     for name, _, _ in arms:
         a, b = statistics.median(times[(name, 0)]), statistics.median(times[(name, 1)])
         print(f"{name}: round-4 epilogue {a:7.1f} us   interleaved {b:7.1f} us   ({(b - a) / a * 100:+.1f} %)", flush=True)
+    # the metric step's dequantise (4096 x 11008 NF4, nested statistics): per-lane vs scalar statistics loads, alone and
+    # in the step (dequantise + k_hgemm, the bench's gemm_4bit call)
+    import ctypes as ct
+    gw = torch.Generator(device=dev).manual_seed(1000)
+    Wm = (torch.randn(4096, 11008, device=dev, generator=gw) * 0.02).to(torch.bfloat16)
+    qm, stm = F.quantize_4bit(Wm, blocksize=64, quant_type="nf4", compress_statistics=True)
+    del Wm
+    Xm = torch.randn(4096, 11008, device=dev, dtype=torch.bfloat16, generator=gw)
+    Ym = torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16)
+    Wd = torch.empty(4096, 11008, device=dev, dtype=torch.bfloat16)
+    deq = lambda: F._dequant_4bit_nested(qm, stm, Wd)  # noqa: E731
+    step = lambda: F.gemm_4bit(Xm, qm, stm, out=Ym)  # noqa: E731
+    outs = []
+    for sq in (0, 1):
+        F.lib.cdequantize_set_nested_scalar(ct.c_int(sq))
+        deq()
+        torch.cuda.synchronize()
+        outs.append(Wd.clone())
+    print(f"dequantise per-lane == scalar stats bitwise: {torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))}",
+          flush=True)
+    td = {0: [], 1: []}
+    ts = {0: [], 1: []}
+    for r in range(rounds):
+        for sq in (0, 1):
+            F.lib.cdequantize_set_nested_scalar(ct.c_int(sq))
+            for _ in range(3):
+                deq()
+            td[sq].append(timed(deq))
+            for _ in range(3):
+                step()
+            ts[sq].append(timed(step))
+    F.lib.cdequantize_set_nested_scalar(ct.c_int(1))
+    print(f"dequantise 4096x11008 nested: per-lane stats {statistics.median(td[0]):6.2f} us   scalar stats "
+          f"{statistics.median(td[1]):6.2f} us   (back to back, same weight)", flush=True)
+    print(f"metric step (gemm_4bit: dequantise + k_hgemm): per-lane stats {statistics.median(ts[0]):7.1f} us   scalar stats "
+          f"{statistics.median(ts[1]):7.1f} us", flush=True)
+    del Xm, Ym, Wd
     # the 33..64-token path as routed (t64 + the reduce launch), graph replay over 14 weight copies
     n_out, k_in = 11008, 4096
     ws = []
     for _ in range(14):
         W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
         ws.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True))
-    import ctypes as ct
     for mrows in (33, 48, 64):
         x = torch.randn(mrows, k_in, device=dev, dtype=torch.bfloat16, generator=g)
         out = torch.empty(mrows, n_out, device=dev, dtype=torch.bfloat16)
