@@ -548,8 +548,10 @@ int g_t64_combine = 0;
 // boundary then has no dirty partials to write back (11008 x 4096 at 64 rows 22.9 -> 21.8 us, 4096 x 11008 24.7 ->
 // 22.3, 4096^2 19.0 -> 15.5; write-through dwords within 0.2 us of the lines; profiles/lab/r04_t64.txt)
 int g_t64_pstore = 2;
-// waves per 48-row set (cgemm_4bit_set_t64_waves): 1 = the round-4 4-wave kernel, 2 = 8 waves, two per SIMD (round 5)
-int g_t64_kp = 1;
+// waves per 48-row set (cgemm_4bit_set_t64_waves): 1 = the round-4 4-wave kernel, 2 = 8 waves, two per SIMD (round 5),
+// 0 = auto: 8 waves up to 48 tokens, 4 above (round 5, 11008 x 4096 nested, graph replay over 14 copies: 33 / 48 / 64
+// rows 20.13 / 21.37 / 21.77 us on 4 waves vs 18.92 / 20.47 / 22.28 on 8; profiles/lab/r05_ab.txt)
+int g_t64_kp = 0;
 
 // this launch's ticket set on the current device (nullptr: use the reduce launch).  Never during HIP-graph capture: a
 // captured launch would bake one ticket set into the graph, and its replays could then share counters with eager
@@ -641,7 +643,7 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
       case 30 + 32 + 64 + 128 + 256: lab(k_gemm_4bit_t64<T, true, 30 + 32 + 64 + 128 + 256>); break;
       default: lab(k_gemm_4bit_t64<T, true>); break;
     }
-  } else if (g_t64_kp == 2) {
+  } else if (g_t64_kp == 2 || (g_t64_kp == 0 && n <= 48)) {
     if (nested)
       hipLaunchKernelGGL((k_gemm_4bit_t64<T, true, 0, 2>), grid, dim3(2 * T64_THREADS), 0, current_stream(), m, n, k, A,
                          lda, B, ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
@@ -684,10 +686,10 @@ int cgemm_4bit_set_t64_pstore(int p) {
   return prev;
 }
 // [additive, testing] waves per 48-row set of the 33..64-token kernel: 1 = 4 waves (one per SIMD), 2 = 8 waves (two per
-// SIMD; round 5); returns the previous setting
+// SIMD; round 5), 0 = auto (8 waves up to 48 tokens); returns the previous setting
 int cgemm_4bit_set_t64_waves(int kp) {
   const int prev = bnb::g_t64_kp;
-  bnb::g_t64_kp = kp == 2 ? 2 : 1;
+  bnb::g_t64_kp = kp == 2 ? 2 : kp == 1 ? 1 : 0;
   return prev;
 }
 int cgemm_4bit_set_t64_combine(int on) {

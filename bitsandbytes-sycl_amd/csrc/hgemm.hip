@@ -1103,9 +1103,15 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   // the dequant epilogue reads 4 column scales / 4 bias halves per 16-B / 8-B load
   if (OP == HG_I8_DEQ && (((uintptr_t)colStats & 15) || ((uintptr_t)bias & 7))) return 1;
   constexpr bool FP = OP == HG_BF16 || OP == HG_FP16;
-  // int8 (HG_I8_DEQ) and the round-3 schedule arm (chgemm_set_variant(1)) run the 256 x 256 tile only
-  const bool full_only = !FP || g_hgemm_variant == 1;
-  if (side && (!FP || g_hgemm_variant == 1)) return 1;
+  // The round-3 schedule arm (chgemm_set_variant(1)) is an A/B arm of the 16-bit kinds only: on the int8 body it is
+  // not deterministic (round 5, tools/r05_diag_int8_variant.py: ~65 k of 16.8 M outputs differ run to run at 4096 x
+  // 4096 x 11008, whole 8-row DMA pieces -- a stage read racing a piece of the two-half schedule; the launched
+  // three-barrier schedule is deterministic and equal to the 8-wave igemm_256 bit for bit), so int8 always runs the
+  // default schedule.
+  const int variant = FP ? g_hgemm_variant : 0;
+  // int8 (HG_I8_DEQ) and the round-3 schedule arm run the 256 x 256 tile only
+  const bool full_only = !FP || variant == 1;
+  if (side && (!FP || variant == 1)) return 1;
   HgPlan pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, FP, full_only);
   if (pl.splits > 1 && (ws == nullptr || ((uintptr_t)ws & 15) ||
                         ws_bytes < (long long)pl.splits * m * n * (long long)sizeof(float)))
@@ -1120,7 +1126,7 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
       else hgemm_launch_shape<OP, VV, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
     }
   };
-  if (g_hgemm_variant == 1) {
+  if (variant == 1) {
     hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
   } else if (g_hg_cwt && g_hg_epi) {
     by_shape(std::integral_constant<int, HG_V | HG_V_CWT | HG_V_EPI>{});

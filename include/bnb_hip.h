@@ -260,7 +260,8 @@ int cgemm_4bit_set_t64_combine(int on);
  * write-through 16-B lines staged through LDS; returns the previous setting */
 int cgemm_4bit_set_t64_pstore(int p);
 /* [additive, testing] that kernel's waves per 48-row set: 1 = 4 waves (one per SIMD), 2 = 8 waves (two per SIMD, the
- * set's blocks alternated between them, partial sums added in LDS); returns the previous setting */
+ * set's blocks alternated between them, partial sums added in LDS), 0 (default) = auto, 8 waves up to 48 activation
+ * rows; returns the previous setting */
 int cgemm_4bit_set_t64_waves(int kp);
 /* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
  * grid_cap = at most that many workgroups (0 = none); returns the previous p */
@@ -269,8 +270,8 @@ int cdequantize_set_stream_cfg(int p, int grid_cap);
  * 2 (default) = device-scope write-through; returns the previous setting */
 int cdequantize_set_store_policy(int policy);
 /* [additive, testing] the nested-statistics dequantise reads each wave's 64 statistic codes and second-level scale by
- * scalar loads (1, default, where blocksize 64 / blocksize2 >= 64 / 64-B aligned codes allow) or per lane (0);
- * bit-identical; returns the previous setting */
+ * scalar loads (1, where blocksize 64 / blocksize2 >= 64 / 64-B aligned codes allow) or per lane (0, default: measured
+ * faster); bit-identical; returns the previous setting */
 int cdequantize_set_nested_scalar(int on);
 /* [additive, testing] k_hgemm side-dequantise A/B bits (chgemm_tn_pf_*); returns the previous value */
 int chgemm_set_side_mode(int v);

@@ -1,6 +1,6 @@
-"""Round 5: the streaming 4-bit dequantise with nested statistics reads each wave's 64 statistic codes and its
-second-level scale by scalar loads (k_dequantize_4bit_stream SQ, cdequantize_set_nested_scalar).  It must equal the
-per-lane form and the oracle bit for bit: whole and ragged tails (waves whose 64 blocks run past the end fall back to
+"""Round 5: the streaming 4-bit dequantise with nested statistics can read each wave's 64 statistic codes and its
+second-level scale by scalar loads (k_dequantize_4bit_stream SQ, cdequantize_set_nested_scalar(1); measured slower, so
+off by default).  It must equal the per-lane form and the oracle bit for bit: whole and ragged tails (waves whose 64 blocks run past the end fall back to
 the per-lane loads), a code array that is not 64-B aligned (the launch keeps the per-lane form), NF4 / FP4, bf16 / fp16,
 and the metric weight through gemm_4bit's dequantise + k_hgemm route."""
 import ctypes as ct
