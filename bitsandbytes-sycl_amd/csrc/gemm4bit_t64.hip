@@ -164,6 +164,15 @@ __device__ __forceinline__ void t64_combine(__amdgpu_buffer_rsrc_t wsr, int ks, 
   }
 }
 
+// lab timeline (ABL 512): per wave 8 s_memrealtime stamps (10 ns ticks) at g_t64_tl[(block * waves + wave) * 8 + i]:
+// start, prologue issued, table built, first half-group landed, loop done, DMA drained, outputs issued, outputs landed
+__device__ unsigned long long* g_t64_tl = nullptr;
+__device__ __forceinline__ unsigned long long t64_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 // N = out features (weight rows), M = tokens (1..64), K = in features (% 256 == 0), blocksize 64.  Workgroup
 // (row tile rt, split sp): rows rt * 192 .., groups [sp * kc, min((sp + 1) * kc, K / 256)).  ksplit > 1: fp32
 // partials ws[sp][token][row], combined by the row tile's last workgroup when `tickets` is given (one counter per row
@@ -198,6 +207,9 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   const int r0 = rt * T64_ROWS + rs * 16 * T64_RG;           // this wave's first weight row
   const int ngr = K >> 8, gr0 = sp * kc, ng = min(kc, ngr - gr0);   // this workgroup's groups (>= 1, host rule)
 
+  constexpr bool TL = (ABL & 512) != 0;
+  unsigned long long tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (TL) tl[0] = t64_now();
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)sm);
   // token pieces: this wave's pieces q = 4 wave + i of a half-group slot; lane l -> token row t = 4 q + (l >> 4),
   // physical 16-B slot p = l & 15 holding logical slot p ^ (t & 15) (k = 8 x logical slot within the 128 k)
@@ -354,6 +366,7 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   issue_t(0, 0);
   issue_t(1, 1);
   issue_w(1, 1);
+  if constexpr (TL) tl[1] = t64_now();
   // ---- the pair table, built while the prologue's DMA is in flight (code values by scalar loads: lgkmcnt, not the
   // vmcnt the DMA counts; the nested code map travels by LDS-DMA with the first pieces)
   if constexpr ((ABL & 64) == 0) {
@@ -375,12 +388,14 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
     }
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);                      // lgkmcnt(0): the table is written (barrier at the wait)
+  if constexpr (TL) tl[2] = t64_now();
 
   for (int gi = 0; gi < ng; ++gi) {
     if constexpr ((ABL & 1) == 0)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(TOPS + WOPS) : "memory");   // T(2 gi) and W(gi) landed (this wave)
     if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();                                          // ... every wave's token pieces
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (TL) tl[3] = gi == 0 ? t64_now() : tl[3];
     consume(gi, 0);
     __builtin_amdgcn_s_waitcnt(0xC07F);                                    // lgkmcnt(0): this wave's reads are done
     if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();                                          // ... every wave's: token slot 0 is free
@@ -397,7 +412,9 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
     issue_t(2 * gi + 3, 1);
     issue_w(gi + 2, gi & 1);
   }
+  if constexpr (TL) tl[4] = t64_now();
   wait_vmcnt0();                                                           // no LDS-DMA may outlive the workgroup
+  if constexpr (TL) tl[5] = t64_now();
 
   // ---- KP = 2: the second wave of each row set hands its partial sums to the first through LDS (the table region, free
   // once every wave is past its last lookup); the first adds them (first + second) and does the stores below
@@ -505,6 +522,15 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
           }
         }
     }
+  }
+
+  if constexpr (TL) {
+    tl[6] = t64_now();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tl[7] = t64_now();
+    if (lane == 0 && g_t64_tl != nullptr)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g_t64_tl[((long long)blockIdx.x * (NT / 64) + wave) * 8 + i] = tl[i];
   }
 
   // ---- split-K combine by the row tile's last workgroup to finish.  Hand-off (the condition the round-2
@@ -640,6 +666,7 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
       case 64: lab(k_gemm_4bit_t64<T, true, 64>); break;
       case 128: lab(k_gemm_4bit_t64<T, true, 128>); break;
       case 256: lab(k_gemm_4bit_t64<T, true, 256>); break;
+      case 512: lab(k_gemm_4bit_t64<T, true, 512>); break;
       case 30 + 32 + 64 + 128 + 256: lab(k_gemm_4bit_t64<T, true, 30 + 32 + 64 + 128 + 256>); break;
       default: lab(k_gemm_4bit_t64<T, true>); break;
     }
@@ -691,6 +718,10 @@ int cgemm_4bit_set_t64_waves(int kp) {
   const int prev = bnb::g_t64_kp;
   bnb::g_t64_kp = kp == 2 ? 2 : kp == 1 ? 1 : 0;
   return prev;
+}
+// [lab, not in the header] timeline buffer of the ABL-512 variant (mode 16 + 512): 8 stamps per wave
+int cgemm_4bit_t64_timeline(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_t64_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
 int cgemm_4bit_set_t64_combine(int on) {
   const int prev = bnb::g_t64_combine;
