@@ -29,7 +29,7 @@ prev = F.lib.cgemm_4bit_set_t64_mode(ct.c_int(16 + 512))
 for it in range(3):
     for i, (q, st) in enumerate(ws):
         if it == 2 and i == 7:
-            F.lib.cgemm_4bit_t64_timeline(ct.c_void_p(F.get_ptr(buf)))
+            F.lib.cgemm_4bit_t64_timeline(F.get_ptr(buf))
         F.gemm_4bit(x, q, st, out=out)
         if it == 2 and i == 7:
             torch.cuda.synchronize()
