@@ -182,6 +182,9 @@ static int g_hg_cwt = 1;
 // conversion overlaps the store stream instead of preceding all of it (chgemm_set_epilogue; round 5)
 constexpr int HG_V_EPI = 65536;
 static int g_hg_epi = 1;
+// variant bit (with HG_V_EPI only): the interleaved epilogue's C stores carry the non-temporal hint (nt), so the output
+// (not re-read by this step) does not displace the operands in the last-level cache (chgemm_set_c_store(2 / 3); lab)
+constexpr int HG_V_CNT = 131072;
 constexpr int HG_V_ALT = 8 + 16 + 4096;
 static int g_hgemm_variant = 0;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
@@ -907,10 +910,9 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       };
       auto store_rows_v = [&](const hg_u32x4_t& v, int it) {
         const int soff = (int)((uint32_t)(RPI * it) * ldc2);
-        if constexpr ((V & HG_V_CWT) != 0)               // device-scope write-through (sc1): no dirty C lines left
-          __builtin_amdgcn_raw_buffer_store_b128(v, cr, (int)loff, soff, 16);
-        else
-          __builtin_amdgcn_raw_buffer_store_b128(v, cr, (int)loff, soff, 0);
+        // device-scope write-through (sc1, 16): no dirty C lines left; nt (2): streaming hint
+        constexpr int AUX = ((V & HG_V_CWT) != 0 ? 16 : 0) | ((V & HG_V_CNT) != 0 ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, cr, (int)loff, soff, AUX);
       };
       hg_u32x4_t pv = {0u, 0u, 0u, 0u};
       int pk = -1;
@@ -1087,7 +1089,7 @@ static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void
       const int steps = pl.kchunk - 1;
       sd.every = steps > 0 ? std::max(1, (steps + sd.iters - 1) / sd.iters) : 1;
       // (the side form keeps the round-4 epilogue: with the side's state live the interleaved one spills)
-      hgemm_launch_side<OP, (V & ~HG_V_EPI), WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
+      hgemm_launch_side<OP, (V & ~(HG_V_EPI | HG_V_CNT)), WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
                                                            ws, sd);
       return;
     }
@@ -1128,6 +1130,9 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   };
   if (variant == 1) {
     hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
+  } else if (g_hg_cwt == 2 && g_hg_epi && pl.wi == 8 && pl.wj == 8) {   // the lab's nt arm: full tile only
+    hgemm_launch_shape<OP, HG_V | HG_V_CWT | HG_V_EPI | HG_V_CNT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats,
+                                                                      colStats, bias, ws, side);
   } else if (g_hg_cwt && g_hg_epi) {
     by_shape(std::integral_constant<int, HG_V | HG_V_CWT | HG_V_EPI>{});
   } else if (g_hg_cwt) {
@@ -1244,10 +1249,10 @@ void chgemm_tn_plan(int m, int n, int k, int* out) {
 }
 // [additive, testing] the side dequantise's A/B bits (HgSide::mode); returns the previous setting
 // [additive, testing] 1 (default): k_hgemm stores C and its split-K partials write-through (sc1), 0: write-back;
-// returns the previous setting
+// 2: write-through + non-temporal (the 256 x 256 tile's interleaved epilogue; others as 1); returns the previous setting
 int chgemm_set_c_store(int wt) {
   const int prev = bnb::g_hg_cwt;
-  bnb::g_hg_cwt = wt ? 1 : 0;
+  bnb::g_hg_cwt = (wt >= 0 && wt <= 2) ? wt : 1;
   return prev;
 }
 // [additive, testing] 1 (default): the interleaved 16-bit epilogue (HG_V_EPI, with write-through C), 0: the round-4 one

@@ -276,7 +276,8 @@ int cdequantize_set_nested_scalar(int on);
 /* [additive, testing] k_hgemm side-dequantise A/B bits (chgemm_tn_pf_*); returns the previous value */
 int chgemm_set_side_mode(int v);
 /* [additive, testing] 1 (default): k_hgemm stores C and its split-K partials write-through (device scope), 0:
- * write-back; returns the previous setting */
+ * write-back, 2: write-through + non-temporal hint (256 x 256 tile, interleaved epilogue; others as 1); returns the
+ * previous setting */
 int chgemm_set_c_store(int wt);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);

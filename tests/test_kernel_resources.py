@@ -14,36 +14,53 @@ CSRC = os.path.join(ROOT, "bitsandbytes-sycl_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
-@pytest.mark.parametrize("src,kernel", [("hgemm.hip", "k_hgemm"), ("probe.hip", "k_probe_mfma")])
-def test_asm_mfma_kernels_compile_spill_free(tmp_path, src, kernel):
-    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-I", CSRC,
-                        "-c", os.path.join(CSRC, src), "-o", str(tmp_path / "k.o"),
-                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=600)
+@pytest.fixture(scope="module")
+def hgemm_device_asm(tmp_path_factory):
+    """hgemm.hip compiled ONCE for the module (device code only, ~5 min): its ISA text and the resource-usage remarks."""
+    if not os.path.exists(HIPCC):
+        pytest.skip("no hipcc")
+    s = tmp_path_factory.mktemp("hgemm") / "k.s"
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                        "-ffp-contract=off", "-I", CSRC, os.path.join(CSRC, "hgemm.hip"), "-o", str(s),
+                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
+    return s.read_text(), r.stderr
+
+
+def _spills(remarks, kernel):
     names, spills = [], []
-    for line in r.stderr.splitlines():
+    for line in remarks.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
         if m:
             names.append(m.group(1))
         m = re.search(r"VGPRs Spill: (\d+)", line)
         if m and names and kernel in names[-1]:
             spills.append((names[-1], int(m.group(1))))
+    return spills
+
+
+def test_hgemm_compiles_spill_free(hgemm_device_asm):
+    spills = _spills(hgemm_device_asm[1], "k_hgemm")
     assert spills, "no kernels found"
     assert all(n == 0 for _, n in spills), spills
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
-def test_hgemm_m0_written_only_by_its_dma_statements(tmp_path):
+def test_probe_compiles_spill_free(tmp_path):
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                        "-ffp-contract=off", "-I", CSRC, os.path.join(CSRC, "probe.hip"), "-o", str(tmp_path / "p.s"),
+                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    spills = _spills(r.stderr, "k_probe_mfma")
+    assert spills, "no kernels found"
+    assert all(n == 0 for _, n in spills), spills
+
+
+def test_hgemm_m0_written_only_by_its_dma_statements(hgemm_device_asm):
     """k_hgemm keeps the LDS-DMA destination in M0 across statements (glds16_chain: one s_add per piece).  That is
     only valid while nothing else in the kernel writes M0: every M0 write in its ISA must be one of the kernel's own
     forms (s_mov_b32 m0, sN / s_add_u32 m0, m0, imm), and no compiler-inserted M0 save or use may appear."""
-    s = tmp_path / "k.s"
-    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                        "-ffp-contract=off", "-I", CSRC, os.path.join(CSRC, "hgemm.hip"), "-o", str(s)],
-                       capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stderr[-2000:]
-    text = s.read_text()
+    text = hgemm_device_asm[0]
     bodies = re.findall(r"^(_ZN3bnb7k_hgemm\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.S | re.M)
     assert bodies, "no k_hgemm kernels"
     for name, body in bodies:
@@ -53,24 +70,18 @@ def test_hgemm_m0_written_only_by_its_dma_statements(tmp_path):
                 assert re.fullmatch(r"s_mov_b32 m0, s\d+|s_add_u32 m0, m0, (0x[0-9a-f]+|\d+)", ins), (name, ins)
 
 
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
-def test_hgemm_tile3_dma_count_between_waits(tmp_path):
+def test_hgemm_tile3_dma_count_between_waits(hgemm_device_asm):
     """The three-barrier k_hgemm schedule (V & 8192) waits `s_waitcnt vmcnt(VM)` once per k-tile, meaning "tile t+1's
     LDS-DMA pieces (issued one k-tile earlier) have landed; the VM issued since may still fly" (256 x 256 tile: 16 pieces,
     VM 13; 256 x 128: 12, 9; 128 x 256: 12, 10).  That count is only right if exactly `pieces` LDS-DMA instructions --
     and no other vector-memory instruction -- sit between two consecutive waits of the steady-state loop, VM of them
     after the k-tile's first barrier.  Checked on the ISA of every launched kind and tile shape (a miscount would let
     fragment reads see a stage before its DMA landed)."""
-    s = tmp_path / "k.s"
-    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                        "-ffp-contract=off", "-I", CSRC, os.path.join(CSRC, "hgemm.hip"), "-o", str(s)],
-                       capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stderr[-2000:]
-    text = s.read_text()
-    bodies = re.findall(r"^(_ZN3bnb7k_hgemmILi\dELi(?:8208|40976|106512)\w+):[^\n]*\n(.*?)^\.Lfunc_end", text,
+    text = hgemm_device_asm[0]
+    bodies = re.findall(r"^(_ZN3bnb7k_hgemmILi\dELi(?:8208|40976|106512|237584)\w+):[^\n]*\n(.*?)^\.Lfunc_end", text,
                         re.S | re.M)
     # (40976 = 8208 | HG_V_CWT: the same loop, C stored write-through; 106512 = 40976 | HG_V_EPI: and the interleaved
-    # epilogue -- the launched kinds)
+    # epilogue -- the launched kinds; 237584 = 106512 | HG_V_CNT: the lab's non-temporal C arm)
     assert any("ELi40976E" in b[0] for b in bodies), "no write-through-C k_hgemm kernels"
     assert any("ELi106512E" in b[0] for b in bodies), "no interleaved-epilogue k_hgemm kernels"
     assert bodies, "no three-barrier k_hgemm kernels"
