@@ -52,6 +52,7 @@ constexpr int T64_TPIECES = 4;                               // token pieces per
 constexpr int T64_STAGE_LD = T64_ROWS + 4;                  // staged partial tile row pitch (floats)
 static_assert(64 * T64_STAGE_LD * 4 <= T64_TABLE, "staged tile fits the table");
 typedef uint32_t hg_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t t64_u32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T> struct T64Mfma;
 template <> struct T64Mfma<bf16_t> {
@@ -557,6 +558,212 @@ k_gemm_4bit_t64(int N, int M, int K, const T* __restrict__ A, int lda, const uin
   }
 }
 
+// ---- The register-fed form (round 5, k_gemm_4bit_t64r): 48 weight rows per workgroup over the WHOLE K, its 4 waves
+// splitting K (wave w: groups [w kc, (w + 1) kc)), every operand loaded straight into VGPRs.
+// Why: the LDS-DMA form above is bound by its in-flight depth -- per CU ~40 KiB in flight in 2-slot LDS rings beside
+// the 64 KiB pair table, a 4-wave barrier per half-group, a reduce launch for the split-K partials (per-wave timeline,
+// profiles/lab/r05_t64_timeline.txt: 9.6 us of loop for 224 KiB per CU, then 5 us of reduce).  Here each wave keeps
+// T64R_D blocks of tokens and weights in flight in its own registers (one wave per SIMD: 512 registers), no barrier
+// runs in the loop, and the K-parts meet in LDS at the end ((p0 + p1) + p2 + p3 -- k_skinny_reduce's order: with the
+// same group split the outputs equal the LDS-DMA form + reduce launch bit for bit).  The price: every workgroup reads
+// all token rows (64 x K x 2 B from L2 per 48 weight rows), so the form needs ~one workgroup per CU from its row tiles
+// alone (host rule).  Arithmetic per block as above: T(code) pairs from the bank-private table into the MFMA, the
+// block's two MFMAs summed in fp32, scaled by the block absmax (one fma per output).
+constexpr int T64R_RG = 3, T64R_ROWS = 16 * T64R_RG, T64R_D = 4;   // rows per workgroup, blocks in flight per wave
+constexpr int T64R_PITCH = T64R_ROWS + 4;                  // combine: floats per token row (conflict-free writes)
+constexpr int T64R_OFF_C2 = T64_TABLE;                      // nested code map (256 floats)
+constexpr int T64R_LDS = T64R_OFF_C2 + 1024;
+static_assert(4 * 64 * T64R_PITCH * 4 <= T64_TABLE, "the four K-part tiles fit the table region");
+
+template <typename T, bool NESTED>
+__global__ void __launch_bounds__(256, 1)
+k_gemm_4bit_t64r(int N, int M, int K, const T* __restrict__ A, int lda, const uint8_t* __restrict__ B, int ldb,
+                 SkStats st, const float* __restrict__ code, T* __restrict__ out, int ldc, int kc) {
+  __shared__ __attribute__((aligned(16))) uint8_t sm[T64R_LDS];
+  uint8_t* table = sm;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * T64R_ROWS;
+  const int ngr = K >> 8, gr0 = min(wave * kc, ngr), ng = min(kc, ngr - gr0);   // this wave's groups (0 for idle parts)
+  const int parts = (ngr + kc - 1) / kc;                     // K-parts holding a partial sum
+  const int nb = 4 * ng;                                     // this wave's blocks
+
+  // tokens: tile mt, lane (n, g) -> token min(16 mt + n, M - 1), k 16 g + 8 s of each block (16 B per s)
+  uint32_t toff[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) toff[mt] = (uint32_t)min(16 * mt + n, M - 1) * (uint32_t)lda * 2u + 32u * (uint32_t)g;
+  // weights: row group rg, lane (n, g) -> row min(r0 + 16 rg + n, N - 1), bytes 8 g .. 8 g + 7 of each block's 32
+  uint32_t woff[T64R_RG], sblk[T64R_RG];
+#pragma unroll
+  for (int rg = 0; rg < T64R_RG; ++rg) {
+    const uint32_t row = (uint32_t)min(r0 + 16 * rg + n, N - 1);
+    woff[rg] = row * (uint32_t)ldb + 8u * (uint32_t)g;
+    sblk[rg] = (uint32_t)(((unsigned long long)row * (unsigned long long)ldb) >> 5);   // the row's first block
+  }
+  const uint8_t* Ab = reinterpret_cast<const uint8_t*>(A);
+  uint4 tb[T64R_D][4][2];
+  t64_u32x2 wb[T64R_D][T64R_RG];
+  auto issue = [&](int bi, auto dtag) {                      // block bi (clamped) of this wave -> ring slot d
+    constexpr int d = decltype(dtag)::value;
+    const long long kb = 4LL * gr0 + min(bi, max(nb - 1, 0));
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) tb[d][mt][s] = *reinterpret_cast<const uint4*>(Ab + 128LL * kb + toff[mt] + 16 * s);
+#pragma unroll
+    for (int rg = 0; rg < T64R_RG; ++rg)
+      wb[d][rg] = __builtin_nontemporal_load(reinterpret_cast<const t64_u32x2*>(B + 32LL * kb + woff[rg]));
+  };
+  // statistics of group gi (clamped): nested -- the 4 block codes (one dword) and the absmax2 of each row; plain -- the
+  // 4 block absmax
+  uint32_t q4[T64R_RG], q4n[T64R_RG];
+  float a2[T64R_RG], a2n[T64R_RG];
+  float4 am[T64R_RG], amn[T64R_RG];
+  auto stats = [&](int gi, uint32_t* q, float* a2v, float4* amv) {
+    const uint32_t G = (uint32_t)(gr0 + min(gi, max(ng - 1, 0)));
+#pragma unroll
+    for (int rg = 0; rg < T64R_RG; ++rg) {
+      const uint32_t j0 = sblk[rg] + 4u * G;
+      if constexpr (NESTED) {
+        q[rg] = *reinterpret_cast<const uint32_t*>(st.q8 + j0);
+        a2v[rg] = st.absmax2[j0 >> st.bs2_shift];
+      } else {
+        amv[rg] = *reinterpret_cast<const float4*>(st.absmax + j0);
+      }
+    }
+  };
+
+  // (the nested code map and offset first: loaded after the ring, their first use would wait for the whole ring)
+  float offset = 0.f;
+  if constexpr (NESTED) {
+    offset = *st.offset;
+    reinterpret_cast<float*>(sm + T64R_OFF_C2)[tid] = st.code2[tid];
+  }
+  static_assert(T64R_D == 4, "one ring slot per block of a 4-block group");
+  if (nb > 0) {
+    issue(0, std::integral_constant<int, 0>{});
+    issue(1, std::integral_constant<int, 1>{});
+    issue(2, std::integral_constant<int, 2>{});
+    issue(3, std::integral_constant<int, 3>{});
+    stats(0, q4, a2, am);
+  }
+  // the pair table {T(code[hi]), T(code[lo])} per packed byte, 32 bank-private copies (the LDS-DMA form's layout)
+  {
+    float dt[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dt[j] = code[j];
+    float hi = dt[0], lo = dt[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      hi = (tid >> 4) == j ? dt[j] : hi;
+      lo = (tid & 15) == j ? dt[j] : lo;
+    }
+    const uint32_t v = Dot2<T>::pair(hi, lo);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(table + 256 * tid + 16 * ((k + tid) & 7)) = make_uint4(v, v, v, v);
+  }
+  __syncthreads();
+  const float* code2s = reinterpret_cast<const float*>(sm + T64R_OFF_C2);
+
+  f32x4_t acc[T64R_RG][4];
+#pragma unroll
+  for (int rg = 0; rg < T64R_RG; ++rg)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[rg][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint32_t lane4 = (uint32_t)(lane & 31) * 4;
+
+  auto consume = [&](auto dtag) {                             // block d of the current group, from ring slot d
+    constexpr int d = decltype(dtag)::value;
+    float a[T64R_RG];
+#pragma unroll
+    for (int rg = 0; rg < T64R_RG; ++rg) {
+      if constexpr (NESTED) a[rg] = __fadd_rn(__fmul_rn(code2s[(q4[rg] >> (8 * d)) & 0xFF], a2[rg]), offset);
+      else a[rg] = d == 0 ? am[rg].x : d == 1 ? am[rg].y : d == 2 ? am[rg].z : am[rg].w;
+    }
+    uint4 bf[T64R_RG][2];
+#pragma unroll
+    for (int rg = 0; rg < T64R_RG; ++rg)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t w = s ? wb[d][rg].y : wb[d][rg].x;
+        uint32_t l[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          l[i] = *reinterpret_cast<const uint32_t*>(table + __builtin_amdgcn_perm(w, lane4, 0x0C0C0000u | ((4u + i) << 8)));
+        bf[rg][s] = make_uint4(l[0], l[1], l[2], l[3]);
+      }
+#pragma unroll
+    for (int rg = 0; rg < T64R_RG; ++rg) {
+      f32x4_t blk[4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          blk[mt] = T64Mfma<T>::mma(tb[d][mt][s], bf[rg][s], s ? blk[mt] : f32x4_t{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[rg][mt][i] = __builtin_fmaf(a[rg], blk[mt][i], acc[rg][mt][i]);
+    }
+  };
+
+  for (int gi = 0; gi < ng; ++gi) {
+    stats(gi + 1, q4n, a2n, amn);                              // the next group's statistics ride with this group
+    const int b0 = 4 * gi + T64R_D;
+    consume(std::integral_constant<int, 0>{});
+    issue(b0 + 0, std::integral_constant<int, 0>{});
+    consume(std::integral_constant<int, 1>{});
+    issue(b0 + 1, std::integral_constant<int, 1>{});
+    consume(std::integral_constant<int, 2>{});
+    issue(b0 + 2, std::integral_constant<int, 2>{});
+    consume(std::integral_constant<int, 3>{});
+    issue(b0 + 3, std::integral_constant<int, 3>{});
+#pragma unroll
+    for (int rg = 0; rg < T64R_RG; ++rg) {
+      q4[rg] = q4n[rg];
+      a2[rg] = a2n[rg];
+      am[rg] = amn[rg];
+    }
+  }
+
+  // ---- the K-parts meet in LDS (the table region: every wave is past its last lookup), then ((p0 + p1) + p2) + p3
+  __syncthreads();
+  float* pb = reinterpret_cast<float*>(sm);
+  if (wave < parts) {
+    float* pw = pb + wave * 64 * T64R_PITCH;
+#pragma unroll
+    for (int rg = 0; rg < T64R_RG; ++rg)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pw[(16 * mt + 4 * g + i) * T64R_PITCH + 16 * rg + n] = acc[rg][mt][i];
+  }
+  __syncthreads();
+  constexpr int C4 = T64R_ROWS / 4;                           // float4 columns of a token row
+  const bool vec = (((uintptr_t)out & 7) == 0) && (ldc & 3) == 0;
+#pragma unroll
+  for (int j = 0; j < (64 * C4) / 256; ++j) {
+    const int e = tid + 256 * j, t = e / C4, c = e - t * C4;
+    if (t >= M) continue;
+    float4 s = *reinterpret_cast<const float4*>(pb + t * T64R_PITCH + 4 * c);
+    for (int p = 1; p < parts; ++p) {
+      const float4 v = *reinterpret_cast<const float4*>(pb + (p * 64 + t) * T64R_PITCH + 4 * c);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const int row = r0 + 4 * c;
+    T* dst = out + (long long)t * ldc + row;
+    if (vec && row + 3 < N) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(t64_cvt2<T>(s.x, s.y), t64_cvt2<T>(s.z, s.w));
+    } else {
+      if (row < N) dst[0] = Io<T>::from_f32(s.x);
+      if (row + 1 < N) dst[1] = Io<T>::from_f32(s.y);
+      if (row + 2 < N) dst[2] = Io<T>::from_f32(s.z);
+      if (row + 3 < N) dst[3] = Io<T>::from_f32(s.w);
+    }
+  }
+}
+
 // One ticket per row tile, in T64_TICKET_SETS sets handed out round-robin to launches, so launches in flight on
 // different streams at the same time do not share counters (every counter is back at zero when its launch ends).
 constexpr int T64_MAX_TILES = 1024, T64_TICKET_SETS = 16;
@@ -575,8 +782,9 @@ int g_t64_combine = 0;
 // 22.3, 4096^2 19.0 -> 15.5; write-through dwords within 0.2 us of the lines; profiles/lab/r04_t64.txt)
 int g_t64_pstore = 2;
 // waves per 48-row set (cgemm_4bit_set_t64_waves): 1 = the round-4 4-wave kernel, 2 = 8 waves, two per SIMD (round 5),
-// 0 = auto: 8 waves up to 48 tokens, 4 above (round 5, 11008 x 4096 nested, graph replay over 14 copies: 33 / 48 / 64
-// rows 20.13 / 21.37 / 21.77 us on 4 waves vs 18.92 / 20.47 / 22.28 on 8; profiles/lab/r05_ab.txt)
+// 0 = auto: 8 waves up to 48 tokens or where K is not split, 4 otherwise (round 5, 11008 x 4096 nested, graph replay over
+// 14 copies: 33 / 48 / 64 rows 20.13 / 21.37 / 21.77 us on 4 waves vs 18.92 / 20.47 / 22.28 on 8, profiles/lab/r05_ab.txt;
+// unsplit 28672 x 8192 at 64 rows 76.4 -> 72.0 us, profiles/lab/r05_t64r_ab.txt)
 int g_t64_kp = 0;
 
 // this launch's ticket set on the current device (nullptr: use the reduce launch).  Never during HIP-graph capture: a
@@ -625,6 +833,21 @@ bool t64_applicable(int m, int n, int k, int lda, int ldb, int blocksize, int bl
          (long long)(m - 1) * ldb + k / 2 < 0xFFFFFFFFLL && (long long)(n - 1) * lda * 2 + 2LL * k < 0x7FFFFFFFLL;
 }
 
+// the register-fed form (k_gemm_4bit_t64r): 1 (default) = off, 2 = wherever the 33..64-token kernel applies, 0 = auto
+// (where its row tiles alone fill >= 3/4 of the CUs).  Off by default: measured 1.4-2.8x slower than the LDS-DMA form +
+// reduce on every shape, growing with the token rows -- every workgroup pulls all 64 x K token values through its
+// vector-memory path, 4x the LDS-DMA form's 64 x K/4 (profiles/lab/r05_t64r_ab.txt; a rotated group order per workgroup,
+// against L2-channel camping of the 16 same-channel token rows of one load, changed nothing)
+int g_t64r = 1;
+static bool t64r_route(int m, int k, const SkStats& st, bool nested) {
+  if (g_t64r == 1 || g_t64_mode >= 15) return false;         // (the LDS-DMA form's labs keep their kernel)
+  if (nested ? ((uintptr_t)st.q8 & 3) != 0 : ((uintptr_t)st.absmax & 15) != 0) return false;
+  if (g_t64r == 2) return true;
+  int cus = device_cu_count();
+  if (cus <= 0) cus = 256;
+  return 4LL * ((m + T64R_ROWS - 1) / T64R_ROWS) >= 3LL * cus;
+}
+
 long long t64_workspace_bytes(int m, int n, int k) {
   if (n < 1 || n > 64 || k < 256 || k % 256) return 0;
   const T64Geom geo = t64_geometry(m, k);
@@ -638,6 +861,18 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
                           long long ws_bytes) {
   const bool nested = st.q8 != nullptr;
   if (!t64_applicable(m, n, k, lda, ldb, blocksize, blocksize2, nested, A, B)) return false;
+  if (t64r_route(m, k, st, nested)) {
+    const int kc = (k / 256 + 3) / 4;
+    const dim3 grid((unsigned)((m + T64R_ROWS - 1) / T64R_ROWS));
+    st.bs_shift = 6;
+    st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc, kc);
+    };
+    if (nested) go(k_gemm_4bit_t64r<T, true>);
+    else go(k_gemm_4bit_t64r<T, false>);
+    return true;
+  }
   const T64Geom geo = t64_geometry(m, k);
   if (geo.ksplit > 1 &&
       (ws == nullptr || ((uintptr_t)ws & 15) || (long long)geo.ksplit * n * m * (long long)sizeof(float) > ws_bytes))
@@ -670,7 +905,7 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
       case 30 + 32 + 64 + 128 + 256: lab(k_gemm_4bit_t64<T, true, 30 + 32 + 64 + 128 + 256>); break;
       default: lab(k_gemm_4bit_t64<T, true>); break;
     }
-  } else if (g_t64_kp == 2 || (g_t64_kp == 0 && n <= 48)) {
+  } else if (g_t64_kp == 2 || (g_t64_kp == 0 && (n <= 48 || geo.ksplit == 1))) {
     if (nested)
       hipLaunchKernelGGL((k_gemm_4bit_t64<T, true, 0, 2>), grid, dim3(2 * T64_THREADS), 0, current_stream(), m, n, k, A,
                          lda, B, ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
@@ -722,6 +957,13 @@ int cgemm_4bit_set_t64_waves(int kp) {
 // [lab, not in the header] timeline buffer of the ABL-512 variant (mode 16 + 512): 8 stamps per wave
 int cgemm_4bit_t64_timeline(unsigned long long* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_t64_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+// [additive, testing] the register-fed 33..64-token form: 0 = auto, 1 = off, 2 = wherever the kernel applies; returns the
+// previous setting
+int cgemm_4bit_set_t64_regfed(int v) {
+  const int prev = bnb::g_t64r;
+  bnb::g_t64r = (v == 1 || v == 2) ? v : 0;
+  return prev;
 }
 int cgemm_4bit_set_t64_combine(int on) {
   const int prev = bnb::g_t64_combine;

@@ -261,8 +261,13 @@ int cgemm_4bit_set_t64_combine(int on);
 int cgemm_4bit_set_t64_pstore(int p);
 /* [additive, testing] that kernel's waves per 48-row set: 1 = 4 waves (one per SIMD), 2 = 8 waves (two per SIMD, the
  * set's blocks alternated between them, partial sums added in LDS), 0 (default) = auto, 8 waves up to 48 activation
- * rows; returns the previous setting */
+ * rows or where K is not split; returns the previous setting */
 int cgemm_4bit_set_t64_waves(int kp);
+/* [additive, testing] that kernel's register-fed form (48 weight rows x whole K per workgroup, the 4 waves splitting K,
+ * operands straight into registers, K-parts summed in LDS: no reduce launch): 1 (default) = off (measured slower), 2 =
+ * wherever the 33..64-token kernel applies, 0 = auto (where its row tiles alone fill >= 3/4 of the CUs); returns the
+ * previous setting */
+int cgemm_4bit_set_t64_regfed(int v);
 /* [additive, testing] launch shape of the 4-bit streaming dequantise: p = packed dwords per lane per pass (4, 8, 16),
  * grid_cap = at most that many workgroups (0 = none); returns the previous p */
 int cdequantize_set_stream_cfg(int p, int grid_cap);
