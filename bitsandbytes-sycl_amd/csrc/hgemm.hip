@@ -185,6 +185,17 @@ static int g_hg_epi = 1;
 // variant bit (with HG_V_EPI only): the interleaved epilogue's C stores carry the non-temporal hint (nt), so the output
 // (not re-read by this step) does not displace the operands in the last-level cache (chgemm_set_c_store(2 / 3); lab)
 constexpr int HG_V_CNT = 131072;
+// variant bit (lab): per-wave s_memrealtime stamps (10 ns ticks) at g_hg_tl[(blockIdx.x * 4 + wave) * 8 + i]: kernel
+// start, prologue done (tile 0 landed, first barrier), k-loop done (DMA drained), epilogue's stores issued, stores
+// complete, the workgroup's tile id (chgemm_timeline; tools/hgemm_timeline.py)
+constexpr int HG_V_TL = 262144;
+__device__ unsigned long long* g_hg_tl = nullptr;
+static int g_hg_tl_on = 0;
+__device__ __forceinline__ unsigned long long hg_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 constexpr int HG_V_ALT = 8 + 16 + 4096;
 static int g_hgemm_variant = 0;
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
@@ -326,6 +337,9 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   // in the prologue so that the epilogue reads them from LDS instead of waiting on global loads
   constexpr int STATS_LDS = (OP == HG_I8_DEQ) ? 4 * BM + 4 * BN + 2 * BN : 0;
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDS_BYTES + SIDE_LDS + STATS_LDS];
+  constexpr bool TL = (V & HG_V_TL) != 0;
+  unsigned long long tl0 = 0, tl1 = 0, tl2 = 0;
+  if constexpr (TL) tl0 = hg_now();
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   using T16 = typename std::conditional<OP == HG_FP16, fp16_t, bf16_t>::type;
@@ -741,6 +755,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     if constexpr (SIDE) __builtin_amdgcn_s_waitcnt(0xC07F);          // (the side tables' LDS writes)
     __builtin_amdgcn_s_barrier();
   }
+  if constexpr (TL) tl1 = hg_now();
 #pragma unroll
   for (int f = 0; f < WJ; ++f) w0[f] = rd(0, wo0, f);
 #pragma unroll
@@ -763,6 +778,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     half2(std::true_type{}, nk - 1, (nk - 1) & 1);
   }
   wait_vmcnt0();                                          // no LDS-DMA may outlive the workgroup
+  if constexpr (TL) tl2 = hg_now();
   // MFMA (asm, invisible to hipcc's hazard recognizer) -> v_accvgpr_read: pad the wait states by hand
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -988,6 +1004,15 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     }
   }
   (void)value;
+  if constexpr (TL) {
+    const unsigned long long tl3 = hg_now();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long tl4 = hg_now();
+    if (lane == 0 && g_hg_tl != nullptr) {
+      unsigned long long* o = g_hg_tl + ((long long)blockIdx.x * 4 + wave) * 8;
+      o[0] = tl0; o[1] = tl1; o[2] = tl2; o[3] = tl3; o[4] = tl4; o[5] = (unsigned long long)wgs;
+    }
+  }
 }
 
 // Host rule: k bytes (k * element size) % 128 == 0, 16-B aligned rows and bases, and every lane offset
@@ -1089,7 +1114,7 @@ static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void
       const int steps = pl.kchunk - 1;
       sd.every = steps > 0 ? std::max(1, (steps + sd.iters - 1) / sd.iters) : 1;
       // (the side form keeps the round-4 epilogue: with the side's state live the interleaved one spills)
-      hgemm_launch_side<OP, (V & ~(HG_V_EPI | HG_V_CNT)), WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
+      hgemm_launch_side<OP, (V & ~(HG_V_EPI | HG_V_CNT | HG_V_TL)), WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
                                                            ws, sd);
       return;
     }
@@ -1130,6 +1155,11 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   };
   if (variant == 1) {
     hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
+  } else if (FP && g_hg_tl_on && g_hg_cwt == 1 && g_hg_epi && pl.wi == 8 && pl.wj == 8 && !side) {   // lab timeline
+    // (16-bit kinds only: on the int8 body the stamps' registers spilled)
+    if constexpr (FP)
+      hgemm_launch_shape<OP, HG_V | HG_V_CWT | HG_V_EPI | HG_V_TL, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats,
+                                                                       colStats, bias, ws, nullptr);
   } else if (g_hg_cwt == 2 && g_hg_epi && pl.wi == 8 && pl.wj == 8) {   // the lab's nt arm: full tile only
     hgemm_launch_shape<OP, HG_V | HG_V_CWT | HG_V_EPI | HG_V_CNT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats,
                                                                       colStats, bias, ws, side);
@@ -1254,6 +1284,11 @@ int chgemm_set_c_store(int wt) {
   const int prev = bnb::g_hg_cwt;
   bnb::g_hg_cwt = (wt >= 0 && wt <= 2) ? wt : 1;
   return prev;
+}
+// [lab, not in the header] per-wave timeline of the 256 x 256 k_hgemm (HG_V_TL): buf = 8 u64 per wave (nullptr: off)
+int chgemm_timeline(unsigned long long* buf) {
+  bnb::g_hg_tl_on = buf != nullptr;
+  return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_hg_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
 // [additive, testing] 1 (default): the interleaved 16-bit epilogue (HG_V_EPI, with write-through C), 0: the round-4 one
 // (convert and stage everything, then store); returns the previous setting
