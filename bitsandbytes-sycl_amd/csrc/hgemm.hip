@@ -187,9 +187,10 @@ static int g_hg_epi = 1;
 constexpr int HG_V_CNT = 131072;
 // variant bit (lab): per-wave s_memrealtime stamps (10 ns ticks) at g_hg_tl[(blockIdx.x * 4 + wave) * 8 + i]: kernel
 // start, prologue done (tile 0 landed, first barrier), k-loop done (DMA drained), epilogue's stores issued, stores
-// complete, the workgroup's tile id (chgemm_timeline; tools/hgemm_timeline.py)
+// complete, the workgroup's tile id, its XCD (chgemm_timeline; tools/hgemm_timeline.py)
 constexpr int HG_V_TL = 262144;
 __device__ unsigned long long* g_hg_tl = nullptr;
+__device__ int g_hg_tl_nswap = 0;      // lab, HG_V_TL only: 1 = each XCD takes the other half of the N-tiles
 static int g_hg_tl_on = 0;
 __device__ __forceinline__ unsigned long long hg_now() {
   unsigned long long t;
@@ -441,7 +442,10 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   const int first_m = (wg / group_span) * GROUP;
   const int gsize = min(tilesM - first_m, GROUP);
   const int tm = first_m + (wg % group_span) % gsize;
-  const int tn = (wg % group_span) / gsize;
+  int tn = (wg % group_span) / gsize;
+  if constexpr (TL) {
+    if (g_hg_tl_nswap) tn = (tn + tilesN / 2) % tilesN;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- DMA: wave w fills A pieces p = WI w + i and B pieces p = WJ w + i (tile rows 8p .. 8p+7); lane -> (row,
@@ -1011,6 +1015,7 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     if (lane == 0 && g_hg_tl != nullptr) {
       unsigned long long* o = g_hg_tl + ((long long)blockIdx.x * 4 + wave) * 8;
       o[0] = tl0; o[1] = tl1; o[2] = tl2; o[3] = tl3; o[4] = tl4; o[5] = (unsigned long long)wgs;
+      o[6] = (unsigned long long)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15);   // HW_REG_XCC_ID: the physical XCD
     }
   }
 }
@@ -1286,6 +1291,9 @@ int chgemm_set_c_store(int wt) {
   return prev;
 }
 // [lab, not in the header] per-wave timeline of the 256 x 256 k_hgemm (HG_V_TL): buf = 8 u64 per wave (nullptr: off)
+int chgemm_timeline_nswap(int v) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_hg_tl_nswap), &v, sizeof(v)) == hipSuccess ? 0 : 1;
+}
 int chgemm_timeline(unsigned long long* buf) {
   bnb::g_hg_tl_on = buf != nullptr;
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_hg_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;

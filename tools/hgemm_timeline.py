@@ -28,9 +28,14 @@ def report(name, buf, nwg):
     for i, nm in enumerate(["prologue", "loop", "epilogue issue", "store drain"]):
         p = np.percentile(d[:, i], [5, 50, 95])
         print(f"   {nm:15s} dur p5 {p[0]:7.2f}  p50 {p[1]:7.2f}  p95 {p[2]:7.2f}", flush=True)
-    # per XCD (tile id % 8 is not the XCD; blockIdx % 8 is): loop-done p50 per XCD
-    xcd = (np.arange(nwg * 4) // 4) % 8
-    print("   loop done p50 per XCD: " + " ".join(f"{np.median(rel[xcd == x, 2]):.2f}" for x in range(8)), flush=True)
+    # by dispatch group (blockIdx % 8: the blocks that share an XCD) and by physical XCD (HW_REG_XCC_ID): if the slow
+    # group moves with the physical XCD across launches it is the hardware, if it stays with blockIdx % 8 the data
+    grp = (np.arange(nwg * 4) // 4) % 8
+    xcc = t[:, 6]
+    print("   loop done p50 by blockIdx % 8: " + " ".join(f"{np.median(rel[grp == x, 2]):.2f}" for x in range(8)), flush=True)
+    print("   loop done p50 by XCC_ID:       " + " ".join(f"{np.median(rel[xcc == x, 2]):.2f}" if (xcc == x).any() else "  -  "
+                                                    for x in range(8)), flush=True)
+    print("   XCC_ID of blockIdx 0..7: " + " ".join(str(int(xcc[4 * b])) for b in range(8)), flush=True)
 
 
 def main():
@@ -49,12 +54,34 @@ def main():
             run()
         ref = Y.clone()
         assert F.lib.chgemm_timeline(ct.c_void_p(buf.data_ptr())) == 0
-        for _ in range(3):
+        for rep in range(3):
             run()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            report(f"bf16 k_hgemm {m}x{n}x{k} (launch {rep})", buf, 256)
         assert F.lib.chgemm_timeline(None) == 0
         assert torch.equal(Y, ref)                       # the timeline variant computes the same bits
-        report(f"bf16 k_hgemm {m}x{n}x{k}", buf, 256)
+    # the same GEMM with each XCD on the other half of the N-tiles (a bijection of the tile map: same outputs): does the
+    # slow group follow the XCD or the data?
+    m, n, k = 4096, 4096, 11008
+    X = torch.randn(m, k, device=dev, dtype=torch.bfloat16, generator=g)
+    W = (torch.randn(n, k, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    Y = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+
+    def run2():
+        F.pre_call(dev)
+        assert F.lib.chgemm_tn_bf16(m, n, k, F.get_ptr(X), k, F.get_ptr(W), k, F.get_ptr(Y), n) == 0
+    for _ in range(3):
+        run2()
+    ref = Y.clone()
+    assert F.lib.chgemm_timeline(ct.c_void_p(buf.data_ptr())) == 0
+    for swap in (0, 1, 0, 1):
+        assert F.lib.chgemm_timeline_nswap(swap) == 0
+        run2()
+        torch.cuda.synchronize()
+        assert torch.equal(Y, ref)
+        report(f"bf16 k_hgemm {m}x{n}x{k}, N halves swapped between XCD pairs: {swap}", buf, 256)
+    assert F.lib.chgemm_timeline_nswap(0) == 0
+    assert F.lib.chgemm_timeline(None) == 0
     # the metric step: dequantise + k_hgemm, the GEMM stamped
     m, n, k = 4096, 4096, 11008
     Wq = (torch.randn(n, k, device=dev, generator=g) * 0.02).to(torch.bfloat16)
