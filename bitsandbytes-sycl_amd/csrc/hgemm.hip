@@ -191,6 +191,7 @@ constexpr int HG_V_CNT = 131072;
 constexpr int HG_V_TL = 262144;
 __device__ unsigned long long* g_hg_tl = nullptr;
 __device__ int g_hg_tl_nswap = 0;      // lab, HG_V_TL only: 1 = each XCD takes the other half of the N-tiles
+__device__ int g_hg_tl_nostore = 0;    // lab, HG_V_TL only: 1 = the interleaved epilogue's C stores are dropped
 static int g_hg_tl_on = 0;
 __device__ __forceinline__ unsigned long long hg_now() {
   unsigned long long t;
@@ -920,7 +921,9 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       // buffer resource on the wave's output corner: one lane-offset VGPR for all of them, the row step in an SGPR (a
       // 64-bit address per store made the 256 x 256 bf16 kind spill here)
       constexpr int SPG = 16 / RPI, EVERY = WJ / SPG;
-      const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, 0x7FFFFFFF, 0x00020000);
+      // (TL lab ablation g_hg_tl_nostore: zero records -- every C store is issued and dropped, no memory write)
+      const int crec = (TL && g_hg_tl_nostore) ? 0 : 0x7FFFFFFF;
+      const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cbase, (short)0, crec, 0x00020000);
       const uint32_t ldc2 = (uint32_t)ldc * 2u;
       const uint32_t loff = (uint32_t)(lane_e / CPR) * ldc2 + 16u * (uint32_t)(lane_e % CPR);
       // store instruction `it` = rows RPI it .. + RPI - 1 of the wave's region; its read-back is issued one slot ahead of
@@ -1293,6 +1296,9 @@ int chgemm_set_c_store(int wt) {
 // [lab, not in the header] per-wave timeline of the 256 x 256 k_hgemm (HG_V_TL): buf = 8 u64 per wave (nullptr: off)
 int chgemm_timeline_nswap(int v) {
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_hg_tl_nswap), &v, sizeof(v)) == hipSuccess ? 0 : 1;
+}
+int chgemm_timeline_nostore(int v) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_hg_tl_nostore), &v, sizeof(v)) == hipSuccess ? 0 : 1;
 }
 int chgemm_timeline(unsigned long long* buf) {
   bnb::g_hg_tl_on = buf != nullptr;

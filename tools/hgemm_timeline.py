@@ -81,6 +81,17 @@ def main():
         assert torch.equal(Y, ref)
         report(f"bf16 k_hgemm {m}x{n}x{k}, N halves swapped between XCD pairs: {swap}", buf, 256)
     assert F.lib.chgemm_timeline_nswap(0) == 0
+    # ablation: the epilogue with its C stores dropped (issued against a zero-record buffer): conversion + staging +
+    # store issue without the memory write -- what the 32 MB write itself costs
+    for nostore in (1, 0):
+        assert F.lib.chgemm_timeline_nostore(nostore) == 0
+        run2()
+        torch.cuda.synchronize()
+        report(f"bf16 k_hgemm {m}x{n}x{k}, C stores dropped: {nostore}", buf, 256)
+    assert F.lib.chgemm_timeline_nostore(0) == 0
+    run2()
+    torch.cuda.synchronize()
+    assert torch.equal(Y, ref)
     assert F.lib.chgemm_timeline(None) == 0
     # the metric step: dequantise + k_hgemm, the GEMM stamped
     m, n, k = 4096, 4096, 11008
