@@ -31,14 +31,17 @@ __global__ void __launch_bounds__(256) k_write(u32x4* __restrict__ dst, long lon
   for (; i < n16; i += stride) st16<POL>(dst + i, v);
 }
 
-// the dequantise's mix: per 16-B load of the source, four 16-B stores (the source index i, the destination 4 i .. 4 i + 3)
+// the dequantise's mix: per 16-B load of the source, four 16-B stores; like the dequantise, every store instruction
+// writes 1 KiB contiguous (a wave's 64 loads at source index i0 + lane go to destination 4 i0 + 64 u + lane)
 template <int POL>
 __global__ void __launch_bounds__(256) k_mix(const u32x4* __restrict__ src, u32x4* __restrict__ dst, long long nsrc16) {
   const long long stride = (long long)gridDim.x * 256;
+  const int lane = threadIdx.x & 63;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nsrc16; i += stride) {
     const u32x4 a = __builtin_nontemporal_load(src + i);
+    const long long i0 = i - lane;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) st16<POL>(dst + 4 * i + u, a + (unsigned)u);
+    for (int u = 0; u < 4; ++u) st16<POL>(dst + 4 * i0 + 64 * u + lane, a + (unsigned)u);
   }
 }
 
