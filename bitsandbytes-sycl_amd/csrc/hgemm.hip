@@ -268,6 +268,18 @@ template <> struct HgPlan3<8, 4> {                      // 256 x 128: 4 B pieces
   }
   __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 23 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
 };
+template <> struct HgPlan3<4, 4> {                      // 128 x 128 (round 5): 32 MFMAs, 4 B + 4 A pieces per wave
+  // step-1 fragments w1 at q 0..3 (B region of the stage), B1 at 5; the 4 B pieces at 6..9 beside x1 at 6..9, B2 at 11;
+  // A pieces at 12, 13; B3 at 14 (vmcnt(6): the previous k-tile's 2 tail A pieces and this k-tile's 4 B + 2 A may
+  // fly); the next tile's step-0 fragments one per 2 MFMAs from 15 to 29 (w0[0] last used at q 3, x0[i] at 12 + i,
+  // w0[j] at 4 j + 3); the last 2 A pieces at 18 and 24.  M0 is set right after a barrier, one MFMA before its piece.
+  static constexpr int B1 = 5, B2 = 11, B3 = 14, SETB = 5, SETA = 11, VM = 6, SIDEQ = 28;
+  __host__ __device__ static constexpr int wread(int q) { return q < 4 ? q : -1; }
+  __host__ __device__ static constexpr int xread(int q) { return q >= 6 && q <= 9 ? q - 6 : -1; }
+  __host__ __device__ static constexpr int bpiece(int q) { return q >= 6 && q <= 9 ? q - 6 : -1; }
+  __host__ __device__ static constexpr int apiece(int q) { return q == 12 ? 0 : q == 13 ? 1 : q == 18 ? 2 : q == 24 ? 3 : -1; }
+  __host__ __device__ static constexpr int nread(int q) { return q > B3 && q <= B3 + 15 && ((q - B3 - 1) & 1) == 0 ? (q - B3 - 1) >> 1 : -1; }
+};
 template <> struct HgPlan3<4, 8> {                      // 128 x 256: 8 B pieces, 4 A pieces per wave
   static constexpr int B1 = 17, B2 = 27, B3 = 38, SETB = 17, SETA = 33, VM = 10, SIDEQ = 58;
   __host__ __device__ static constexpr int wread(int q) { return q < 16 && (q & 1) == 0 ? q >> 1 : -1; }
@@ -1048,21 +1060,29 @@ long long hgemm_tiles(int m, int n) { return (long long)((m + HG_BM - 1) / HG_BM
 // tools/route_probe3.py, profiles/lab/r04_routes_before.txt).
 constexpr int HG_SPLIT_TILES = 192, HG_SPLIT_MIN_KT = 8, HG_SPLIT_MAX = 8;
 constexpr double HG_HALF_KT = 0.6;
+// the 128 x 128 tile (round 5, 16-bit kinds, no side dequantise): a quarter of the 256 x 256 tile's MFMAs per k-tile with
+// twice its copies and fragment reads per MFMA; its k-tile time in 256 x 256 k-tile units (lab-calibrated,
+// chgemm_set_quarter_tile)
+static double g_hg_quarter_kt = 0.40;
+static int g_hg_quarter = 1;             // 0 = never, 1 = by cost (default), 2 = forced where allowed (tests / A-B)
 struct HgPlan {
   int wi, wj, splits, kchunk;
 };
 int device_cu_count();   // CUs of the current device (cached; gemv4bit.hip)
-static HgPlan hgemm_plan(int m, int n, int k, int elem, bool allow_split, bool full_tiles_only) {
+static HgPlan hgemm_plan(int m, int n, int k, int elem, bool allow_split, bool full_tiles_only,
+                         bool allow_quarter = false) {
   const int nkt = (int)((long long)k * elem / 128);
   int cus = device_cu_count();
   if (cus <= 0) cus = 256;
   const double part_kt = (double)m * n * 8.0 / 5.0e12 / 1.37e-6;   // one split's partial traffic, in k-tile times
-  static const int shapes[3][2] = {{8, 8}, {8, 4}, {4, 8}};
+  static const int shapes[4][2] = {{8, 8}, {8, 4}, {4, 8}, {4, 4}};
+  const bool quarter = allow_quarter && !full_tiles_only && g_hg_quarter != 0;
+  const bool forced = quarter && g_hg_quarter == 2;
   HgPlan best{8, 8, 1, nkt};
   double best_cost = 1e300;
-  for (int si = 0; si < (full_tiles_only ? 1 : 3); ++si) {
+  for (int si = forced ? 3 : 0; si < (full_tiles_only ? 1 : quarter ? 4 : 3); ++si) {
     const int wi = shapes[si][0], wj = shapes[si][1];
-    const double tkt = (wi == 8 && wj == 8) ? 1.0 : HG_HALF_KT;
+    const double tkt = (wi == 8 && wj == 8) ? 1.0 : (wi == 4 && wj == 4) ? g_hg_quarter_kt : HG_HALF_KT;
     const long long tiles = (long long)((m + 32 * wi - 1) / (32 * wi)) * ((n + 32 * wj - 1) / (32 * wj));
     double cost = (double)((tiles + cus - 1) / cus) * nkt * tkt;
     if (cost < best_cost) {
@@ -1084,7 +1104,7 @@ static HgPlan hgemm_plan(int m, int n, int k, int elem, bool allow_split, bool f
   return best;
 }
 long long hgemm_workspace_bytes(int m, int n, int k, int elem) {
-  const HgPlan pl = hgemm_plan(m, n, k, elem, true, false);
+  const HgPlan pl = hgemm_plan(m, n, k, elem, true, false, elem == 2);
   return pl.splits > 1 ? (long long)pl.splits * m * n * (long long)sizeof(float) : 0;
 }
 
@@ -1110,7 +1130,7 @@ template <int OP, int V, int WI, int WJ>
 static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
                                long long ldb, void* C, long long ldc, const float* rowStats, const float* colStats,
                                const fp16_t* bias, float* ws, const HgSide* side) {
-  if constexpr ((OP == HG_BF16 || OP == HG_FP16) && (V & 8192) != 0) {
+  if constexpr ((OP == HG_BF16 || OP == HG_FP16) && (V & 8192) != 0 && !(WI == 4 && WJ == 4)) {
     if (side) {
       const long long wgs = (long long)((m + 32 * WI - 1) / (32 * WI)) * ((n + 32 * WJ - 1) / (32 * WJ)) * pl.splits;
       HgSide sd = *side;
@@ -1147,10 +1167,12 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   // int8 (HG_I8_DEQ) and the round-3 schedule arm run the 256 x 256 tile only
   const bool full_only = !FP || variant == 1;
   if (side && (!FP || variant == 1)) return 1;
-  HgPlan pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, FP, full_only);
+  // (the 128 x 128 tile: 16-bit kinds without a side dequantise -- the side form is not built for it)
+  const bool quarter = FP && side == nullptr;
+  HgPlan pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, FP, full_only, quarter);
   if (pl.splits > 1 && (ws == nullptr || ((uintptr_t)ws & 15) ||
                         ws_bytes < (long long)pl.splits * m * n * (long long)sizeof(float)))
-    pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, false, full_only);      // no (large enough) workspace: no split
+    pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, false, full_only, quarter);   // no (large enough) workspace: no split
   // variant bits of the launched kernel: write-through C (g_hg_cwt) and the interleaved epilogue (g_hg_epi, with it)
   auto by_shape = [&](auto vtag) {
     constexpr int VV = decltype(vtag)::value;
@@ -1158,7 +1180,8 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
       hgemm_launch_shape<OP, VV, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
     else if constexpr (FP) {
       if (pl.wi == 8) hgemm_launch_shape<OP, VV, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-      else hgemm_launch_shape<OP, VV, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+      else if (pl.wj == 8) hgemm_launch_shape<OP, VV, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+      else hgemm_launch_shape<OP, VV, 4, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
     }
   };
   if (variant == 1) {
@@ -1279,7 +1302,7 @@ long long chgemm_tn_workspace_bytes(int m, int n, int k) { return bnb::hgemm_wor
 // k-tiles per split}; the output tile is 32 WI x 32 WJ (256 x 256, 256 x 128 or 128 x 256)
 void chgemm_tn_plan(int m, int n, int k, int* out) {
   BNB_RANGE("chgemm_tn_plan");
-  const bnb::HgPlan pl = bnb::hgemm_plan(m, n, k, 2, true, bnb::g_hgemm_variant == 1);
+  const bnb::HgPlan pl = bnb::hgemm_plan(m, n, k, 2, true, bnb::g_hgemm_variant == 1, true);
   out[0] = pl.wi;
   out[1] = pl.wj;
   out[2] = pl.splits;
@@ -1291,6 +1314,15 @@ void chgemm_tn_plan(int m, int n, int k, int* out) {
 int chgemm_set_c_store(int wt) {
   const int prev = bnb::g_hg_cwt;
   bnb::g_hg_cwt = (wt >= 0 && wt <= 2) ? wt : 1;
+  return prev;
+}
+// [additive, testing] the 128 x 128 tile of the 16-bit k_hgemm: mode 0 = never, 1 = by the plan's cost (default), 2 = forced
+// wherever allowed; kt_x1000 > 0 sets its k-tile time in 256 x 256 k-tile units x 1000 (the cost model); returns the
+// previous mode
+int chgemm_set_quarter_tile(int mode, int kt_x1000) {
+  const int prev = bnb::g_hg_quarter;
+  bnb::g_hg_quarter = (mode >= 0 && mode <= 2) ? mode : 1;
+  if (kt_x1000 > 0) bnb::g_hg_quarter_kt = kt_x1000 / 1000.0;
   return prev;
 }
 // [lab, not in the header] per-wave timeline of the 256 x 256 k_hgemm (HG_V_TL): buf = 8 u64 per wave (nullptr: off)

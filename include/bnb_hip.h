@@ -284,6 +284,10 @@ int chgemm_set_side_mode(int v);
  * write-back, 2: write-through + non-temporal hint (256 x 256 tile, interleaved epilogue; others as 1); returns the
  * previous setting */
 int chgemm_set_c_store(int wt);
+/* [additive, testing] the 128 x 128 tile of the 16-bit k_hgemm (round 5): mode 0 = never, 1 = by the launch plan's cost
+ * (default), 2 = forced wherever allowed (no side dequantise); kt_x1000 > 0 sets the tile's k-tile time for the cost
+ * model (256 x 256 k-tile units x 1000); returns the previous mode */
+int chgemm_set_quarter_tile(int mode, int kt_x1000);
 /* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
 int chgemm_set_variant(int v);
 /* [additive, testing] k_hgemm's 16-bit epilogue: 1 (default) = interleaved per 16-row group (conversion overlapped with

@@ -263,12 +263,13 @@ def test_hgemm_schedule_variants_bit_identical(dev, mnk):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("mnk,plan", [((2048, 4096, 4096), (8, 4, 1)), ((96, 11008, 4096), (4, 8, 5)),
-                                      ((4096, 1024, 8192), (8, 4, 2)), ((128, 8192, 8192), (4, 8, 8)),
+                                      ((4096, 1024, 8192), (8, 4, 2)), ((128, 8192, 8192), (4, 4, 4)),
                                       ((300, 700, 1024), None), ((2051, 1037, 640), None), ((4096, 4096, 2048), (8, 8, 1))])
 def test_hgemm_tile_shapes_against_fp32_product(dev, dtype, mnk, plan):
     """The half-width tiles (256 x 128 and 128 x 256, picked by the launch plan for grids that a 256 x 256 tiling leaves
-    half empty or rows that waste half a 256-row tile), with and without split-K, ragged edges included: against the
-    fp32 product (the module's contract) and deterministic; chgemm_tn_plan reports the plan the shape takes."""
+    half empty or rows that waste half a 256-row tile) and, since round 5, the 128 x 128 tile (128 x 8192 x 8192: 4
+    splits of 64 tiles instead of 8 of 32), with and without split-K, ragged edges included: against the fp32 product
+    (the module's contract) and deterministic; chgemm_tn_plan reports the plan the shape takes."""
     F = _F()
     m, n, k = mnk
     out4 = (ct.c_int * 4)()
@@ -285,3 +286,37 @@ def test_hgemm_tile_shapes_against_fp32_product(dev, dtype, mnk, plan):
     rc2, Y2 = _hgemm_ws(F, X, W)
     torch.cuda.synchronize()
     assert rc2 == 0 and torch.equal(Y, Y2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mnk", [(4096, 512, 11008), (4096, 128, 8192), (300, 260, 576), (2051, 1037, 640),
+                                 (129, 130, 64), (4096, 1024, 8192), (1, 3, 128)])
+def test_hgemm_quarter_tile_against_fp32_product(dev, dtype, mnk):
+    """The 128 x 128 tile (round 5; chgemm_set_quarter_tile(2) forces it): with the workspace its plan asks for (split-K
+    on small grids) and without (unsplit), ragged edges included, against the fp32 product and deterministic; unsplit it
+    runs the same MFMA sequence per output block as the 256 x 256 kernel, so its bits equal chgemm_tn_*'s."""
+    F = _F()
+    m, n, k = mnk
+    g = torch.Generator(device=dev).manual_seed(m + 3 * n + k)
+    X = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    W = (torch.rand(n, k, device=dev, generator=g) * 2 - 1).to(dtype)
+    rc0, Yfull = _hgemm(F, X, W)                        # the unsplit 256 x 256 kernel
+    prev = F.lib.chgemm_set_quarter_tile(ct.c_int(2), ct.c_int(0))
+    try:
+        plan = (ct.c_int * 4)()
+        F.lib.chgemm_tn_plan(m, n, k, plan)
+        assert tuple(plan[:2]) == (4, 4), tuple(plan)
+        rc1, Y = _hgemm_ws(F, X, W)
+        rc2, Y2 = _hgemm_ws(F, X, W)
+        fn = F.lib.chgemm_tn_ws_bf16 if dtype == torch.bfloat16 else F.lib.chgemm_tn_ws_fp16
+        Yu = torch.empty(m, n, device=dev, dtype=dtype)
+        F.pre_call(dev)
+        rc3 = fn(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k), F.get_ptr(X), ct.c_int32(k), F.get_ptr(W), ct.c_int32(k),
+                 F.get_ptr(Yu), ct.c_int32(n), F.get_ptr(None), ct.c_longlong(0))   # no workspace: unsplit 128 x 128
+        torch.cuda.synchronize()
+    finally:
+        F.lib.chgemm_set_quarter_tile(ct.c_int(prev), ct.c_int(0))
+    assert rc0 == 0 and rc1 == 0 and rc2 == 0 and rc3 == 0
+    _check(Y, X, W)
+    assert torch.equal(Y, Y2)
+    assert torch.equal(Yu, Yfull)

@@ -73,7 +73,7 @@ def test_hgemm_m0_written_only_by_its_dma_statements(hgemm_device_asm):
 def test_hgemm_tile3_dma_count_between_waits(hgemm_device_asm):
     """The three-barrier k_hgemm schedule (V & 8192) waits `s_waitcnt vmcnt(VM)` once per k-tile, meaning "tile t+1's
     LDS-DMA pieces (issued one k-tile earlier) have landed; the VM issued since may still fly" (256 x 256 tile: 16 pieces,
-    VM 13; 256 x 128: 12, 9; 128 x 256: 12, 10).  That count is only right if exactly `pieces` LDS-DMA instructions --
+    VM 13; 256 x 128: 12, 9; 128 x 256: 12, 10; 128 x 128: 8, 6).  That count is only right if exactly `pieces` LDS-DMA instructions --
     and no other vector-memory instruction -- sit between two consecutive waits of the steady-state loop, VM of them
     after the k-tile's first barrier.  Checked on the ISA of every launched kind and tile shape (a miscount would let
     fragment reads see a stage before its DMA landed)."""
@@ -87,7 +87,7 @@ def test_hgemm_tile3_dma_count_between_waits(hgemm_device_asm):
     assert bodies, "no three-barrier k_hgemm kernels"
     vmem = re.compile(r"^\s*(global_|buffer_|flat_|scratch_)")
     # per tile shape (WI, WJ): LDS-DMA pieces per k-tile and the vmcnt of barrier B3 (HgPlan3 in hgemm.hip)
-    plans = {(8, 8): (16, 13), (8, 4): (12, 9), (4, 8): (12, 10)}
+    plans = {(8, 8): (16, 13), (8, 4): (12, 9), (4, 8): (12, 10), (4, 4): (8, 6)}
     shapes_seen = set()
     side_seen = False
     for name, body in bodies:
