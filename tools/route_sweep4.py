@@ -13,7 +13,7 @@ import python_src_quants.functional as F  # noqa: E402
 WEIGHTS = [(4096, 4096), (11008, 4096), (4096, 11008), (1024, 8192), (3584, 8192), (1024, 28672), (512, 11008),
            (128, 8192), (8192, 8192)]
 ROWS = [96, 128, 256, 512, 1024, 2048]
-ROUTES = ["hgemm", "fused", "library_tn"]
+ROUTES = ["hgemm", "fused", "library_tn", "hgemm_no_quarter"]   # (round 5: the last = hgemm without the 128 x 128 tile)
 
 
 def timed(fn, reps=5):
@@ -36,13 +36,22 @@ def main():
         for M in ROWS:
             X = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
             out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            def call(r):
+                if r == "hgemm_no_quarter":
+                    prev = F.lib.chgemm_set_quarter_tile(0, 0)
+                    try:
+                        F.gemm_4bit(X, q, st, out=out, _route="hgemm")
+                    finally:
+                        F.lib.chgemm_set_quarter_tile(prev, 0)
+                else:
+                    F.gemm_4bit(X, q, st, out=out, _route=r)
             for r in ROUTES:
-                F.gemm_4bit(X, q, st, out=out, _route=r)
+                call(r)
             torch.cuda.synchronize()
             res = {r: [] for r in ROUTES}
             for _ in range(3):
                 for r in ROUTES:
-                    res[r].append(timed(lambda r=r: F.gemm_4bit(X, q, st, out=out, _route=r)))
+                    res[r].append(timed(lambda r=r: call(r)))
             med = {r: sorted(v)[1] for r, v in res.items()}
             best = min(med, key=med.get)
             print(f"{M:6d}x{N:6d}x{K:6d} static {F.gemm_4bit_static_route(M, N, K):7s} best {best:10s} " +
