@@ -1104,8 +1104,11 @@ static HgPlan hgemm_plan(int m, int n, int k, int elem, bool allow_split, bool f
   return best;
 }
 long long hgemm_workspace_bytes(int m, int n, int k, int elem) {
-  const HgPlan pl = hgemm_plan(m, n, k, elem, true, false, elem == 2);
-  return pl.splits > 1 ? (long long)pl.splits * m * n * (long long)sizeof(float) : 0;
+  // the larger of the plans with and without the 128 x 128 tile: a side-dequantise launch (chgemm_tn_pf_*) plans
+  // without it and must find its partials' room too
+  const HgPlan pq = hgemm_plan(m, n, k, elem, true, false, elem == 2), pn = hgemm_plan(m, n, k, elem, true, false, false);
+  const int splits = std::max(pq.splits, pn.splits);
+  return splits > 1 ? (long long)splits * m * n * (long long)sizeof(float) : 0;
 }
 
 // side: the next weight's dequantise to run inside this launch (nullptr: none); its per-workgroup share and step spacing

@@ -182,8 +182,8 @@ def test_int8_on_the_4wave_kernel_is_bit_identical(dev, mnk):
 def test_hgemm_split_k_against_fp32_product(dev, dtype, mnk):
     """Small tile grids through chgemm_tn_ws_*: split-K (when the launch plan picks it) over fp32 partials in the
     caller's workspace, summed in split order -- within the same fp32-product bound as the unsplit kernel (the k order
-    differs, the accumulation is fp32 either way), deterministic across calls, and the workspace query matches the
-    plan (0 when the shape is not split); a too-small workspace runs the best unsplit plan."""
+    differs, the accumulation is fp32 either way), deterministic across calls, and the workspace query covers the
+    plan; a too-small workspace runs the best unsplit plan."""
     F = _F()
     m, n, k = mnk
     g = torch.Generator(device=dev).manual_seed(m + n + k)
@@ -192,7 +192,9 @@ def test_hgemm_split_k_against_fp32_product(dev, dtype, mnk):
     nbytes = int(F.lib.chgemm_tn_workspace_bytes(ct.c_int32(m), ct.c_int32(n), ct.c_int32(k)))
     plan = (ct.c_int * 4)()
     F.lib.chgemm_tn_plan(m, n, k, plan)
-    assert nbytes == (plan[2] * m * n * 4 if plan[2] > 1 else 0), (tuple(plan), nbytes)
+    # (the query covers the plan and, since round 5, the plan without the 128 x 128 tile that a side-dequantise launch
+    # takes: at least the chosen plan's partials)
+    assert nbytes >= (plan[2] * m * n * 4 if plan[2] > 1 else 0), (tuple(plan), nbytes)
     ws = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=dev)
     fn = F.lib.chgemm_tn_ws_bf16 if dtype == torch.bfloat16 else F.lib.chgemm_tn_ws_fp16
     outs = []
