@@ -937,9 +937,11 @@ def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
     """The deterministic route of a (rows, N, K) product (round 4, tools/route_sweep4.py, profiles/lab/r04_route_sweep.txt):
       * up to GEMM_4BIT_FEW_TOKENS rows: "fused" (the few-token kernels and the multi-row GEMV, picked inside);
       * the one-kernel fused NF4 GEMM ("fused") where the weight is deep and wide and the rows few -- K >= 8192 and
-        N >= 4096 up to 512 rows (4096 x 11008 at 96..256 rows 45-55 us vs 54-62 dequantise + k_hgemm; 8192 x 8192
-        53-96 vs 69-100), K >= 16384 at 257..1024 rows (1024 x 28672 at 1024 rows 85 vs 102): there the bf16 weight's
-        write + read costs more than the fused kernel's in-LDS dequantisation;
+        N >= 4096 up to 384 rows (4096 x 11008 at 96..256 rows 45-55 us vs 50-59 dequantise + k_hgemm; 8192 x 8192
+        52-65 vs 62-86), K >= 16384 at 513..1024 rows (1024 x 28672 at 1024 rows 84 vs 100): there the bf16 weight's
+        write + read costs more than the fused kernel's in-LDS dequantisation.  Round 5 (the 128 x 128 k_hgemm tile,
+        profiles/lab/r05_route_sweep.txt): at 512 rows the pair is ahead or level (4096 x 11008 73-80 vs 81; 8192 x
+        8192 97 vs 97; 1024 x 28672 64 vs 69), so the band ends at 384 / starts above 512;
       * everywhere else the dequantise + the hand-written k_hgemm ("hgemm"; 256 x 256 / 256 x 128 / 128 x 256 tiles and
         split-K by its launch plan); operands beyond one launch's 32-bit offsets (prompts above ~195k tokens at K =
         11008, weights above 2^31 elements) run it in row / weight chunks (_gemm_4bit_hgemm_chunked).  "library" only
@@ -950,7 +952,7 @@ def gemm_4bit_static_route(rows: int, N: int, K: int) -> str:
     if rows <= GEMM_4BIT_FEW_TOKENS:
         return "fused"
     if rows < GEMM_4BIT_DEQUANT_MIN_ROWS:
-        if (K >= 8192 and N >= 4096 and rows <= 512) or (K >= 16384 and 256 < rows <= 1024):
+        if (K >= 8192 and N >= 4096 and rows <= 384) or (K >= 16384 and 512 < rows <= 1024):
             return "fused"
     return "hgemm" if K % 64 == 0 else "library"
 
