@@ -264,6 +264,9 @@ k_gemv_4bit_dot(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
 // LDS: 64 KiB table + 2K activations (the nested code map sits in the table's spare halves): two workgroups per CU
 // up to K = 8192 (exactly half the CU's LDS each), one workgroup of up to 16 waves per CU above that (K <= 16384).
 constexpr int GB_TABLE_BYTES = 65536;
+// nested statistics decoded where each chunk is consumed (LAZY, round 5) or all up front (the round-4 form; A/B knob
+// cgemv_4bit_set_lazy_nested)
+static int g_gv_lazy = 1;
 constexpr int GB_MAX_WAVES = 16;
 // two workgroups per CU up to 79 KiB (K <= 7680), and at exactly half the CU's 160 KiB (K = 8192) from 2048 rows:
 // 3584 / 4096 / 8192 x 8192 6.20 / 6.79 / 10.77 -> 6.00 / 6.34 / 10.43 us, but 1024 x 8192 4.00 -> 5.04 us, where
@@ -272,7 +275,7 @@ static size_t g_gb_two_per_cu_lds = 79 * 1024;
 constexpr size_t GB_HALF_CU_LDS = 80 * 1024;
 constexpr int GB_HALF_CU_MIN_ROWS = 2048;
 
-template <typename T, int R, int U, bool NESTED>
+template <typename T, int R, int U, bool NESTED, bool LAZY = true>
 __global__ void __launch_bounds__(GB_MAX_WAVES * 64)
 k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
                 const float* __restrict__ datatype, T* __restrict__ out, int ldb, int G) {
@@ -355,7 +358,9 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * U) : "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
-  if constexpr (NESTED) {
+  // (nested, LAZY: each block's absmax is decoded where its chunk is consumed, so the code-map reads and the decode of
+  // later chunks overlap the lookups of earlier ones instead of all preceding the first dot)
+  if constexpr (NESTED && !LAZY) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -389,6 +394,7 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
         s0 = Dot2<T>::dot(x[i], l[i], s0);
         s1 = Dot2<T>::dot(x[i + 1], l[i + 1], s1);
       }
+      if constexpr (NESTED && LAZY) am[u][j] = __fadd_rn(__fmul_rn(code2s_at(q8[u][j]), a2[u][j]), offset);
       const float part = (s0 + s1) * am[u][j];
       acc[j] += valid ? part : 0.0f;
     }
@@ -601,23 +607,30 @@ static bool launch_gemv_bal(int m, int k, const T* A, const uint8_t* B, const Ge
     hipLaunchKernelGGL(kern, dim3(G), dim3(64 * nw), lds, current_stream(), m, k, A, B, st, datatype, out, ldb, G);
     return true;
   };
-  switch (R * 8 + U) {
-    case 8 + 1: return go(k_gemv_4bit_bal<T, 1, 1, NESTED>);
-    case 8 + 2: return go(k_gemv_4bit_bal<T, 1, 2, NESTED>);
-    case 8 + 3: return go(k_gemv_4bit_bal<T, 1, 3, NESTED>);
-    case 8 + 4: return go(k_gemv_4bit_bal<T, 1, 4, NESTED>);
-    case 8 + 6: return go(k_gemv_4bit_bal<T, 1, 6, NESTED>);
-    case 8 + 8: return go(k_gemv_4bit_bal<T, 1, 8, NESTED>);
-    case 16 + 1: return go(k_gemv_4bit_bal<T, 2, 1, NESTED>);
-    case 16 + 2: return go(k_gemv_4bit_bal<T, 2, 2, NESTED>);
-    case 16 + 3: return go(k_gemv_4bit_bal<T, 2, 3, NESTED>);
-    case 16 + 4: return go(k_gemv_4bit_bal<T, 2, 4, NESTED>);
-    case 24 + 1: return go(k_gemv_4bit_bal<T, 3, 1, NESTED>);
-    case 24 + 2: return go(k_gemv_4bit_bal<T, 3, 2, NESTED>);
-    case 32 + 1: return go(k_gemv_4bit_bal<T, 4, 1, NESTED>);
-    case 32 + 2: return go(k_gemv_4bit_bal<T, 4, 2, NESTED>);
-    default: return false;
+  auto pick = [&](auto lz) {
+    constexpr bool LZ = decltype(lz)::value;
+    switch (R * 8 + U) {
+      case 8 + 1: return go(k_gemv_4bit_bal<T, 1, 1, NESTED, LZ>);
+      case 8 + 2: return go(k_gemv_4bit_bal<T, 1, 2, NESTED, LZ>);
+      case 8 + 3: return go(k_gemv_4bit_bal<T, 1, 3, NESTED, LZ>);
+      case 8 + 4: return go(k_gemv_4bit_bal<T, 1, 4, NESTED, LZ>);
+      case 8 + 6: return go(k_gemv_4bit_bal<T, 1, 6, NESTED, LZ>);
+      case 8 + 8: return go(k_gemv_4bit_bal<T, 1, 8, NESTED, LZ>);
+      case 16 + 1: return go(k_gemv_4bit_bal<T, 2, 1, NESTED, LZ>);
+      case 16 + 2: return go(k_gemv_4bit_bal<T, 2, 2, NESTED, LZ>);
+      case 16 + 3: return go(k_gemv_4bit_bal<T, 2, 3, NESTED, LZ>);
+      case 16 + 4: return go(k_gemv_4bit_bal<T, 2, 4, NESTED, LZ>);
+      case 24 + 1: return go(k_gemv_4bit_bal<T, 3, 1, NESTED, LZ>);
+      case 24 + 2: return go(k_gemv_4bit_bal<T, 3, 2, NESTED, LZ>);
+      case 32 + 1: return go(k_gemv_4bit_bal<T, 4, 1, NESTED, LZ>);
+      case 32 + 2: return go(k_gemv_4bit_bal<T, 4, 2, NESTED, LZ>);
+      default: return false;
+    }
+  };
+  if constexpr (NESTED) {
+    if (!g_gv_lazy) return pick(std::false_type{});
   }
+  return pick(std::true_type{});
 }
 
 
@@ -759,10 +772,17 @@ void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
 void cgemv_4bit_set_wide_rows(int mode) { bnb::g_gemv_wide_rows = mode; }
 // [lab, not in the header] LDS bytes up to which the balanced GEMV runs two workgroups per CU (default 80 KiB)
 void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size_t)bytes; }
+// [additive, testing] nested statistics of the balanced GEMV decoded where each chunk is consumed (1, default) or all
+// before the first dot (0, the round-4 form); bit-identical; returns the previous setting
+int cgemv_4bit_set_lazy_nested(int on) {
+  const int prev = bnb::g_gv_lazy;
+  bnb::g_gv_lazy = on ? 1 : 0;
+  return prev;
+}
 
 void cgemm_4bit_inference_naive_fp16(int m, int n, int k, fp16_t* A, unsigned char* B, float* absmax, float* datatype,
                                      fp16_t* out, int lda, int ldb, int ldc, int blocksize) {
-  BNB_RANGE("cgemv_4bit_set_kernel");
+  BNB_RANGE("cgemm_4bit_inference_naive_fp16");
   gemv_4bit<fp16_t>(m, n, k, A, B, absmax, datatype, out, lda, ldb, ldc, blocksize);
 }
 void cgemm_4bit_inference_naive_bf16(int m, int n, int k, bf16_t* A, unsigned char* B, float* absmax, float* datatype,
