@@ -264,9 +264,10 @@ k_gemv_4bit_dot(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
 // LDS: 64 KiB table + 2K activations (the nested code map sits in the table's spare halves): two workgroups per CU
 // up to K = 8192 (exactly half the CU's LDS each), one workgroup of up to 16 waves per CU above that (K <= 16384).
 constexpr int GB_TABLE_BYTES = 65536;
-// nested statistics decoded where each chunk is consumed (LAZY, round 5) or all up front (the round-4 form; A/B knob
-// cgemv_4bit_set_lazy_nested)
-static int g_gv_lazy = 1;
+// nested statistics decoded where each chunk is consumed (LAZY, round 5) or all up front (the round-4 form, default; A/B
+// knob cgemv_4bit_set_lazy_nested).  Measured and rejected: bit-identical, +0.2..+1.9 % (11008 x 4096 8.25 -> 8.34 us;
+// tools/r05_gemv_lazy_ab.py, profiles/lab/r05_gemv_lazy_ab.txt)
+static int g_gv_lazy = 0;
 constexpr int GB_MAX_WAVES = 16;
 // two workgroups per CU up to 79 KiB (K <= 7680), and at exactly half the CU's 160 KiB (K = 8192) from 2048 rows:
 // 3584 / 4096 / 8192 x 8192 6.20 / 6.79 / 10.77 -> 6.00 / 6.34 / 10.43 us, but 1024 x 8192 4.00 -> 5.04 us, where
@@ -772,8 +773,8 @@ void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
 void cgemv_4bit_set_wide_rows(int mode) { bnb::g_gemv_wide_rows = mode; }
 // [lab, not in the header] LDS bytes up to which the balanced GEMV runs two workgroups per CU (default 80 KiB)
 void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size_t)bytes; }
-// [additive, testing] nested statistics of the balanced GEMV decoded where each chunk is consumed (1, default) or all
-// before the first dot (0, the round-4 form); bit-identical; returns the previous setting
+// [additive, testing] nested statistics of the balanced GEMV decoded where each chunk is consumed (1) or all before the
+// first dot (0, default: measured faster); bit-identical; returns the previous setting
 int cgemv_4bit_set_lazy_nested(int on) {
   const int prev = bnb::g_gv_lazy;
   bnb::g_gv_lazy = on ? 1 : 0;

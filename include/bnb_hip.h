@@ -102,8 +102,8 @@ int cgemm_4bit_fewtok_takes(int m, int n, int k, int blocksize);
 /* [additive, testing] GEMV kernel choice: 0 = auto (the balanced-range kernel where the shape fits, else the
  * 4-waves-x-R-rows kernel), 1 = the 4-waves-x-R-rows kernel only; both give identical bits */
 void cgemv_4bit_set_kernel(int which);
-/* [additive, testing] the balanced GEMV's nested statistics decoded per chunk where it is consumed (1, default; round 5)
- * or all before the first dot (0); bit-identical; returns the previous setting */
+/* [additive, testing] the balanced GEMV's nested statistics decoded per chunk where it is consumed (1; round 5, measured
+ * 0.2-1.9 % slower) or all before the first dot (0, default); bit-identical; returns the previous setting */
 int cgemv_4bit_set_lazy_nested(int on);
 /* [additive, testing] 1 = the wide GEMV (narrow / long-K weights) one row per workgroup; 0 = rows per workgroup
    by the launch rule (up to 4, sharing one activation load and table fill) */
