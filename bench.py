@@ -211,6 +211,216 @@ def auto_chunks(world, requested=0):
     return 1 if world >= 8 else 2
 
 
+# ---------------------------------------------------------------------------------------------------------------------
+# Self-validation of the N > 1 step: a broken all-gather must not print a TFLOP/s number.  After the
+# timed region every rank checks the step's own outputs:
+#   (a) its shard Y_r equals its column block of the assembled [M, N] output BIT FOR BIT (an all-gather is a copy);
+#   (b) the assembled output is the same on every rank (a position-weighted checksum of its bits, MIN == MAX);
+#   (c) rank 0 recomputes a sample of rows of the world-1 product on the FULL weight and compares (NF4: within the
+#       GEMM tolerance -- the product is not row-split invariant; int8: bit for bit -- exact int32 and a
+#       per-element epilogue).
+# Results are combined over ranks (SUM / MIN / MAX all-reduces), so every rank reaches the same verdict; main() exits
+# non-zero on any mismatch after rank 0 printed the line (outputs_verified false).
+
+GEMM_RTOL = 2e-2        # the GEMM tolerance of the parity tests: |d| <= atol + rtol |ref|,
+GEMM_ATOL_RMS = 2e-2    # atol = 2e-2 * rms(ref) for bf16
+
+
+def _bits(t):
+    """The raw bits of a tensor as integers of the same width (bitwise comparison: -0 != +0, NaN == NaN)."""
+    t = t.contiguous()
+    return t.view({1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[t.element_size()])
+
+
+def _dist_on() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def _reduce_int(v, op, dev):
+    if not _dist_on():
+        return int(v)
+    t = torch.tensor([int(v)], device=dev, dtype=torch.int64)
+    dist.all_reduce(t, op=op)
+    return int(t.item())
+
+
+def bits_checksum(a) -> int:
+    """Position-weighted sum of the bits of `a` (int64, no overflow below ~2^37 16-bit elements): two tensors with the
+    same checksum on every rank are, for this check's purpose, the same tensor."""
+    b = _bits(a).reshape(-1)
+    total, step = 0, 1 << 24
+    for s in range(0, b.numel(), step):
+        part = b[s:s + step].to(torch.int64)
+        w = torch.arange(s, s + part.numel(), device=part.device, dtype=torch.int64) % 65521 + 1
+        total += int((part * w).sum().item())
+    return total
+
+
+def sample_rows(m, count=64):
+    """`count` token rows spread over [0, m), first and last included."""
+    count = min(count, m)
+    return sorted({round(i * (m - 1) / max(1, count - 1)) for i in range(count)})
+
+
+def within_tolerance(got, ref, rtol=GEMM_RTOL, atol_rms=GEMM_ATOL_RMS) -> dict:
+    """The GEMM tolerance of the parity tests, as a dict for the JSON line."""
+    ref = ref.float()
+    d = (got.float() - ref).abs()
+    atol = atol_rms * float(ref.pow(2).mean().sqrt())
+    bad = int((~(d <= atol + rtol * ref.abs())).sum().item())
+    return {"ok": bad == 0, "violations": bad, "max_abs_err": float(d.max()), "atol": atol, "rtol": rtol}
+
+
+def verify_sharded_output(y_local, assembled, world, rank, dev, sample_fn=None) -> dict:
+    """Checks (a)-(c) above for one sharded step.  y_local [M, n]: this rank's output shard; assembled [M, world * n]:
+    this rank's copy of the gathered output; sample_fn(assembled) -> dict with "ok" (run on rank 0 only).  Every rank
+    takes part in the same collectives whatever its local result, and gets the same combined verdict."""
+    n = y_local.shape[1]
+    blk = assembled[:, rank * n:(rank + 1) * n]
+    mism = int((_bits(blk) != _bits(y_local)).sum().item())
+    ck = bits_checksum(assembled)
+    sample, sample_ok = None, 1
+    if rank == 0 and sample_fn is not None:
+        try:
+            sample = sample_fn(assembled)
+        except Exception as ex:  # noqa: BLE001 - a failing check is a failed verification, not a hang of the others
+            sample = {"ok": False, "error": repr(ex)}
+        sample_ok = int(bool(sample.get("ok")))
+    mism_all = _reduce_int(mism, dist.ReduceOp.SUM, dev)
+    same = _reduce_int(ck, dist.ReduceOp.MIN, dev) == _reduce_int(ck, dist.ReduceOp.MAX, dev)
+    sample_ok = _reduce_int(sample_ok, dist.ReduceOp.MIN, dev)
+    res = {"ok": mism_all == 0 and same and sample_ok == 1, "shard_block_mismatches": mism_all,
+           "assembled_identical_on_all_ranks": same, "world1_sample_ok": bool(sample_ok)}
+    if sample is not None:
+        res["world1_sample"] = sample
+    return res
+
+
+def nf4_world1_sample(X, q_full, st_full, rows):
+    """sample_fn for the NF4 step: the sampled rows of the assembled output against (1) the world-1 product of the
+    product path (gemm_4bit on the full weight) and (2) an fp32 product of the dequantised full weight (dequantize_4bit is
+    bit-exact against the oracle), both within the GEMM tolerance."""
+    idx = torch.tensor(rows, device=X.device)
+    xs = X.index_select(0, idx).contiguous()
+    y1 = F.gemm_4bit(xs, q_full, st_full)
+    Wd = F.dequantize_4bit(q_full, st_full).float()
+    ref = xs.float() @ Wd.t()
+    del Wd
+
+    def check(assembled):
+        got = assembled.index_select(0, idx)
+        a, b = within_tolerance(got, ref), within_tolerance(got, y1)
+        return {"rows": len(rows), "ok": a["ok"] and b["ok"], "vs_fp32_of_dequantized_weight": a,
+                "vs_world1_gemm_4bit": b}
+    return check
+
+
+def int8_world1_sample(A, CB_full, SCB_full, rows):
+    """sample_fn for the int8 leg: the world-1 fused igemmlt + dequant of the sampled rows on the FULL CB; int32 is exact
+    and the dequant is per element, so the assembled rows must equal it bit for bit."""
+    idx = torch.tensor(rows, device=A.device)
+    ca, sca = F.int8_row_quant(A.index_select(0, idx).contiguous())
+    y1 = F.igemmlt_dequant(ca, CB_full, sca, SCB_full)
+
+    def check(assembled):
+        got = assembled.index_select(0, idx)
+        mism = int((_bits(got) != _bits(y1)).sum().item())
+        return {"rows": len(rows), "ok": mism == 0, "bitwise_mismatches_vs_world1": mism}
+    return check
+
+
+def time_allgather(y_chunk, out_chunk, chunks, world, dev, iters=20) -> dict:
+    """The step's all-gather alone: `chunks` gathers of one [Mc, n] shard chunk per step (the step's own buffers and
+    backend), barrier-bracketed, max over ranks.  Bytes: what every rank receives ((world - 1) shards) per step."""
+    from python_src_quants.parallel import _gather_async
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+    for _ in range(3):
+        _gather_async(out_chunk, y_chunk).wait()
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        for _ in range(chunks):
+            _gather_async(out_chunk, y_chunk).wait()
+    sync()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per = t.item() / iters
+    shard_bytes = y_chunk.numel() * y_chunk.element_size() * chunks
+    recv = shard_bytes * (world - 1)
+    return {"us_per_step": per * 1e6, "bytes_received_per_rank_per_step": recv,
+            "bytes_assembled_per_rank_per_step": shard_bytes * world, "chunks": chunks,
+            "recv_gbs_per_rank": recv / per / 1e9,
+            "note": "the step's own all-gathers alone (own timing, not the overlapped step); max over ranks"}
+
+
+def dist_info(dev) -> dict:
+    """What the communicator and the devices report: backend, world size, and every rank's device (PCI id, name) --
+    N distinct GPUs expected on the driver's multi-GPU node."""
+    me = {"rank": dist.get_rank(), "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid()}
+    if dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        me.update({"device": dev.index, "name": p.name,
+                   "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+                   "uuid": str(getattr(p, "uuid", ""))})
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me)
+    pcis = [r.get("pci") for r in ranks]
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": ranks,
+            "distinct_gpus": len(set(pcis)) if None not in pcis else 0}
+
+
+def backend_label() -> str:
+    """The process group's backend as the line names it ("RCCL" for torch's "nccl" on ROCm)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return "none"
+    b = dist.get_backend()
+    return "RCCL" if b == "nccl" else b
+
+
+def verify_check_cpu(args, world, rank) -> int:
+    """--verify-check: the N > 1 self-validation on CPU tensors over gloo (no GPU): the real sharded step helper
+    (parallel.sharded_forward_overlapped) on an fp32 toy GEMM, then verify_sharded_output.  --corrupt MODE injects a
+    fault on rank --corrupt-rank: "shard" (its own output changed after the gather: check a), "assembled" (its copy of
+    another rank's block: check b), "values" (its shard computed from a perturbed weight, gathered consistently: only the
+    world-1 sample, check c, sees it).  Prints rank 0's verdict as JSON; returns the exit status (3 = mismatch)."""
+    from python_src_quants.parallel import sharded_forward_overlapped
+    dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    m, n_out, k = 64, 32 * world, 128
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(m, k, generator=g)
+    W = torch.randn(n_out, k, generator=g) * 0.05
+    n = n_out // world
+    Wr = W[rank * n:(rank + 1) * n].clone()
+    if args.corrupt == "values" and rank == args.corrupt_rank:
+        Wr[0, 0] += 1.0
+    chunks = 2
+    Y = torch.empty(m, n)
+    gathered = torch.empty(chunks, world, m // chunks, n)
+    full = torch.empty(m, n_out)
+    sharded_forward_overlapped(X, lambda xc, yc: torch.matmul(xc, Wr.t(), out=yc), world, None, chunks,
+                               out=gathered, y=Y, rows_out=full)
+    if args.corrupt == "shard" and rank == args.corrupt_rank:
+        Y[3, 1] += 1.0
+    if args.corrupt == "assembled" and rank == args.corrupt_rank:
+        other = (rank + 1) % world
+        full[5, other * n] += 1.0
+    rows = sample_rows(m, 16)
+    ref = X[rows] @ W.t()
+    res = verify_sharded_output(Y, full, world, rank, dev,
+                                sample_fn=lambda a: within_tolerance(a[rows], ref))
+    info = dist_info(dev)
+    if rank == 0:
+        print(json.dumps({"outputs_verified": res["ok"], "verification": res, "distributed": info}), flush=True)
+    dist.destroy_process_group()
+    return 0 if res["ok"] else 3
+
+
 def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
     """The metric's INT8 half at 1/2/4/8 GPUs: Linear8bitLt's CB/SCB [n, k] sharded by output
     feature (ColumnShardedLinear8bitLt, rows of CB), the fp16 activations replicated and row-quantised on every
@@ -223,6 +433,8 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
     CB, _, SCB, _, _ = F.double_quant(Wt)
     del Wt
     lin = ColumnShardedLinear8bitLt(CB, SCB, world, rank)
+    # rank 0 keeps the full CB / SCB for the world-1 sample check after the timed region (verify_sharded_output)
+    check = int8_world1_sample(A, CB, SCB, sample_rows(m)) if world > 1 and rank == 0 else None
     del CB
     clock = StepClock(steps)
 
@@ -254,11 +466,20 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
     per = elapsed / steps
     ops = 2.0 * m * n * k
     med = clock.median_ms() * 1e-3
-    return {"shape": [m, n, k], "n_gpus": world, "tops": ops / per / 1e12, "ms_per_step": per * 1e3,
-            "median_step_ms_rank0": med * 1e3,
-            "step": "int8_row_quant(X) + fused igemmlt+dequant on this rank's CB rows" +
-                    (f" + RCCL all_gather ({chunks} chunks) + [M, N] assembly" if world > 1 else ""),
-            "frac_of_int8_peak": ops / per / 1e12 / PEAK_INT8_TOPS}
+    res = {"shape": [m, n, k], "n_gpus": world, "tops": ops / per / 1e12, "ms_per_step": per * 1e3,
+           "median_step_ms_rank0": med * 1e3,
+           "step": "int8_row_quant(X) + fused igemmlt+dequant on this rank's CB rows" +
+                   (f" + {backend_label()} all_gather ({chunks} chunks) + [M, N] assembly" if world > 1 else ""),
+           "frac_of_int8_peak": ops / per / 1e12 / PEAK_INT8_TOPS}
+    if world > 1:
+        # the step once more, outside the timed region, its outputs checked: this rank's rows alone (bit-exact whatever
+        # the chunking: exact int32, per-element dequant) against its block of the assembled output
+        assembled = lin.forward(A, assemble=True, chunks=chunks)
+        local = lin.forward_local(A)
+        torch.cuda.synchronize()
+        res["verification"] = verify_sharded_output(local, assembled, world, rank, dev, sample_fn=check)
+        res["outputs_verified"] = res["verification"]["ok"]
+    return res
 
 
 def bench_decode_sharded(dev, world, rank, steps, warmup, gather="rccl"):
@@ -278,9 +499,12 @@ def bench_decode_sharded(dev, world, rank, steps, warmup, gather="rccl"):
     del W
     lin = ColumnShardedLinear4bit.from_quantized(q, st, world, rank)
     lin.qweight = lin.qweight.clone()
+    x_check = torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g)
+    ref_row = None
+    if world > 1 and rank == 0:    # the world-1 row of x_check (fp32 product of the dequantised full weight)
+        ref_row = x_check.float() @ F.dequantize_4bit(q, st).float().t()
     del q
     dec = lin.decode_step(gather=gather)
-    x_check = torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g)
     dec.set_input(x_check)
     graph = dec.capture()
     if world > 1:
@@ -313,13 +537,22 @@ def bench_decode_sharded(dev, world, rank, steps, warmup, gather="rccl"):
            "weight_bytes_per_rank": wbytes, "rank_weight_gbs": wbytes / per / 1e9,
            "step": "gemv_4bit on this rank's rows" + (
                " + one-shot peer-memory all-gather (IpcAllGather, one kernel) into the [1, N] row" if gather == "ipc"
-               else " written into its slice of the [1, N] row + in-place RCCL all_gather_into_tensor" if world > 1
+               else f" written into its slice of the [1, N] row + in-place {backend_label()} all_gather" if world > 1
                else " written straight into the [1, N] row (one kernel)"),
            "note": "host wall per replayed step (barrier-bracketed, max over ranks): the latency a decode token pays "
                    "for this one layer, including the graph launch"}
     dec.set_input(x_check)
     res["_row"] = dec().clone()
     torch.cuda.synchronize()
+    if world > 1:
+        # the assembled row against this rank's GEMV run on its own (same kernel and shape: bitwise), identical on every
+        # rank, and (rank 0) against the world-1 row within the GEMM tolerance
+        own = F.gemv_4bit(x_check, lin.qweight.t(), state=lin.quant_state)
+        torch.cuda.synchronize()
+        res["verification"] = verify_sharded_output(
+            own, res["_row"], world, rank, dev,
+            sample_fn=(lambda a: within_tolerance(a, ref_row)) if ref_row is not None else None)
+        res["outputs_verified"] = res["verification"]["ok"]
     if dec.ipc is not None:
         res["ipc_timeouts"] = dec.ipc.timeouts()
         res["ipc_memory"] = dec.ipc.memory_kind
@@ -842,6 +1075,11 @@ def main():
     ap.add_argument("--chunks", type=int, default=0,
                     help="N>1: token-row chunks whose all-gathers overlap the next chunk's GEMM (0 = auto: 2 at 2 and "
                          "4 GPUs, 1 at 8 -- see auto_chunks)")
+    ap.add_argument("--verify-check", action="store_true",
+                    help="N>1 output self-validation on CPU tensors over gloo (no GPU); exits 3 on a mismatch")
+    ap.add_argument("--corrupt", default="none", choices=("none", "shard", "assembled", "values"),
+                    help="--verify-check: the fault to inject (see verify_check_cpu)")
+    ap.add_argument("--corrupt-rank", type=int, default=1)
     ap.add_argument("--launch-check", action="store_true",
                     help="print the rank layout (every rank over gloo, no GPU work) and exit: checks the N-rank launch")
     args = ap.parse_args()
@@ -853,6 +1091,10 @@ def main():
                          f"bench.py: world size {world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.verify_check:
+        if world < 2:
+            raise SystemExit("bench.py --verify-check needs --gpus N >= 2")
+        sys.exit(verify_check_cpu(args, world, rank))
     if args.launch_check:
         # the rank layout only (no GPU): every rank joins a gloo group and rank 0 prints who took part
         if world > 1:
@@ -887,6 +1129,8 @@ def main():
     q_full, st_full = F.quantize_4bit(W, blocksize=BS, quant_type="nf4", compress_statistics=True)
     del W
     q, st = shard_quantized_4bit(q_full, st_full, world, rank)
+    # rank 0: the world-1 sample check after the timed region (verify_sharded_output) needs the full weight
+    nf4_check = nf4_world1_sample(X, q_full, st_full, sample_rows(M)) if rank == 0 else None
     if world > 1:
         q = q.clone()
         del q_full
@@ -980,6 +1224,16 @@ def main():
 
     median_step_ms = clock.median_ms()
 
+    # N > 1: the step's own outputs checked (the last timed step's Y and assembled [M, N]), the communicator and the
+    # devices recorded, the all-gather timed alone -- all outside the timed region
+    verification, dinfo, allgather = None, None, None
+    torch.cuda.synchronize()
+    verification = verify_sharded_output(Y, full_out if world > 1 else Y, world, rank, dev, sample_fn=nf4_check)
+    if world > 1:
+        dinfo = dist_info(dev)
+        allgather = time_allgather(Y[:Mc], gathered[0], chunks, world, dev)
+        allgather["backend"] = backend_label()
+
     extras = {}
     if not args.no_int8:     # every rank: it contains collectives when world > 1
         extras["int8_igemmlt_sharded"] = bench_int8_sharded(dev, world, rank, args.steps, args.warmup, chunks)
@@ -1024,6 +1278,13 @@ def main():
         except Exception as ex:  # noqa: BLE001
             cpu = {"value": None, "unit": "TFLOP/s", "cores": None, "kind": "port", "sample": f"failed: {ex}"}
 
+    # every rank holds the same combined verdicts (verify_sharded_output all-reduces them)
+    legs = {"nf4_step": verification}
+    if world > 1:
+        for key in ("int8_igemmlt_sharded", "decode_sharded_config2"):
+            if key in extras:
+                legs[key] = extras[key].get("verification")
+    bad_legs = [k for k, v in legs.items() if not (v and v.get("ok"))]
     if rank == 0 and peaks and "int8_mfma_tops" in peaks:
         for key in ("int8_igemmlt_sharded", "int8_igemmlt_metric_shape", "int8_igemmlt_config3"):
             if key in extras and "tops" in extras[key]:
@@ -1055,7 +1316,7 @@ def main():
                                       "(--prefetch)" if PREFETCH[0] else ", every step dequantising its weight") +
                                    ")" + (" + bf16 all-gather of output-column shards" if world > 1 else ""),
                        "M": M, "N": N, "K": K, "blocksize": BS, "quant_type": "nf4", "compress_statistics": True,
-                       "parallelism": (f"column-shard x{world} + RCCL all_gather, {chunks} token-row chunks "
+                       "parallelism": (f"column-shard x{world} + {backend_label()} all_gather, {chunks} token-row chunks "
                                        "(chunk c's all-gather overlaps chunk c+1's GEMM; the step ends with the [M, N] "
                                        "output assembled)") if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -1072,10 +1333,20 @@ def main():
             "measured_peaks": peaks,
             "cpu_baseline": cpu,
         }
+        line["verification"] = verification
+        if world > 1:
+            line["distributed"] = dinfo
+            line["allgather"] = allgather
+        line["outputs_verified"] = not bad_legs
+        if bad_legs:
+            line["verification_failed"] = bad_legs
         line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if bad_legs:
+        print(f"bench.py: output verification FAILED on {bad_legs} (rank {rank})", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

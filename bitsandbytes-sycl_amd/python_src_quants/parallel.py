@@ -374,11 +374,25 @@ class IpcAllGather:
         return int(self.state[1].item())
 
     def check(self):
-        """Raise when any step of this exchange timed out (its rows, and every later step's, are NaN)."""
+        """Raise when any step of this exchange timed out (its rows, and every later step's, are NaN).  Local: a rank can
+        raise here while a peer that finished cleanly carries on -- between ranks use check_all()."""
         n = self.timeouts()
         if n:
             raise RuntimeError(f"IpcAllGather: {n} peer wait(s) timed out (last source rank "
                                f"{int(self.state[2].item()) - 1}); the gathered rows are poisoned (NaN)")
+
+    def check_all(self):
+        """check() agreed over the group (a collective: every rank must call it): timeouts are asymmetric -- rank A can
+        give up on a slow peer B while B later finds A's flag and finishes cleanly -- so the ranks' counts are reduced
+        (MAX) first and then every rank raises, or none does (a lone raise left the healthy ranks waiting in
+        the next collective until the process-group timeout)."""
+        n = self.timeouts()
+        dev = torch.device("cpu") if dist.get_backend(self.group) == "gloo" else self.device
+        t = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        if int(t.item()):
+            raise RuntimeError(f"IpcAllGather: peer wait(s) timed out on {'this rank' if n else 'a peer rank'} "
+                               f"(max {int(t.item())} per rank); the gathered rows are poisoned (NaN)")
 
     def close(self, barrier: bool = True):
         """Unmap the peers' buffers and free this rank's, after every rank stopped pushing (a barrier)."""
@@ -479,19 +493,21 @@ class ShardedDecode:
             torch.cuda.current_stream(self.x.device).wait_stream(s)
             torch.cuda.synchronize(self.x.device)
             if ipc:
-                self.ipc.check()
-                self._barrier()
+                self.ipc.check_all()      # every rank raises together, or none (a collective; also the barrier)
             g = torch.cuda.CUDAGraph()
+            captured = True
             try:
                 with torch.cuda.graph(g):
                     self.step()
             except Exception:  # noqa: BLE001 - capture refused: stay eager
                 torch.cuda.synchronize(self.x.device)
-                return False
+                captured = False
         finally:
             self.checked = checked
         if ipc:
-            self.ipc.check()
+            self.ipc.check_all()          # reached on every rank, captured or not
+        if not captured:
+            return False
         self.graph = g
         return True
 

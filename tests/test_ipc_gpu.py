@@ -141,6 +141,12 @@ def _timeout_worker(rank, world, port, ret):
             res["latched_nan"] = bool(torch.isnan(rows.float()).all())
             res["timeouts_after"] = ag.timeouts()
         dist.barrier()
+        try:                                       # the agreed check: rank 1 timed out nowhere, yet raises too
+            ag.check_all()
+            res["all_raised"] = False
+        except RuntimeError:
+            res["all_raised"] = True
+        dist.barrier()
         ag.close()
     except Exception as ex:  # noqa: BLE001
         res["error"] = repr(ex)
@@ -163,6 +169,7 @@ def test_ipc_allgather_timeout_poisons_row():
     assert r0["nan_row"] and r0["timeouts"] >= 1 and r0["raised"], r0
     assert r0["latched_nan"] and r0["timeouts_after"] == r0["timeouts"], r0
     assert r0["latched_s"] < 0.25 * r0["wait_s"], r0
+    assert all(got[r]["all_raised"] for r in range(world)), got     # check_all: every rank raises together
 
 
 def test_ipc_allgather_two_processes_one_gpu():
