@@ -79,6 +79,9 @@ def launch_ranks(argv) -> None:
     if "WORLD_SIZE" in os.environ or _gpus_arg(argv) <= 1:
         return
     env = dict(os.environ)
+    # The hosts of this pool support only dmabuf IPC; HSA_ENABLE_IPC_MODE_LEGACY=0 selects it (the images export it
+    # already, here and on the GPU box, so the driver's own torchrun line runs with the same value).  Kept for a launch
+    # from a stripped environment: without it RCCL / hipIpc handles fail with 'hipIpcGetMemHandle: invalid argument'.
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     rc = subprocess.call(rank_launch_cmd(argv, _free_port()), env=env)
     sys.exit(rc)
@@ -898,11 +901,14 @@ def host_cpu_info():
             "torch_threads": torch.get_num_threads()}
 
 
-def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
+def cpu_baseline(rows=M, budget_s=12.0, max_reps=40):
     """Reference CPU path as ported (oracle/cpu_ops_port.cpp, the restated cpu_ops.cpp dequantize_cpu,
     single-threaded as written) + torch CPU F.linear (the CPU path has no GEMM), on a
     bounded sample: per repetition the full W [4096, 11008] is dequantised and multiplied with `rows`
-    activation rows; repetitions run until ~budget_s of CPU work, the median rep is reported.  Beside it,
+    activation rows (all M = 4096 by default: the whole metric product, no extrapolation); repetitions run until
+    ~budget_s of CPU work, the median rep is reported.  Threads: torch's, i.e. the job's CPU share on the box (the pool
+    sets OMP_NUM_THREADS to the per-GPU share, 16; the machine's other cores belong to other jobs' GPUs, so taking them
+    would measure a neighbour's slowdown, not this baseline).  Beside it,
     config 1 itself (NF4 4096 x 4096, bs 64, one index byte per element) through the port and through the
     product's host entry point cdequantize_blockwise_cpu_fp32 (csrc/cpu_ops.cpp, multi-threaded)."""
     import numpy as np
@@ -955,7 +961,8 @@ def cpu_baseline(rows=1024, budget_s=12.0, max_reps=40):
     return {"value": value, "unit": "TFLOP/s", "cores": threads, "kind": "port",
             "sample": f"{len(deq)} reps of: dequantize_cpu (1 thread, as ref:sycl/cpu_ops.cpp:7-14) of W[{N},{K}] "
                       f"NF4 bs=64 unpacked ({t_deq:.3f}s, {n_el * 9 / t_deq / 1e9:.2f} GB/s) + torch CPU fp32 "
-                      f"F.linear on {rows} of the {M} rows ({t_mm:.3f}s, {threads} torch threads); median rep",
+                      f"F.linear on {rows} of the {M} rows ({t_mm:.3f}s, {threads} torch threads = the job's CPU "
+                      f"share, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}); median rep",
             "cores_per_leg": {"dequantize_cpu": 1, "torch_linear": threads},
             "host": host_cpu_info(),
             "dequant_cpu_gbs": n_el * 9 / t_deq / 1e9,

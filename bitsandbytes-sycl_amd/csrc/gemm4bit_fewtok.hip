@@ -49,7 +49,7 @@ __device__ __forceinline__ unsigned long long ft_now() {
   return t;
 }
 
-constexpr int FT_THREADS = 256;
+[[maybe_unused]] constexpr int FT_THREADS = 256;
 // pair table: entry e of bank-private copy c at byte 256 e + 4 c (32 copies, 64 KiB span) so that a lookup address is
 // ONE v_perm_b32 of {packed dword, lane byte}; the nested code map sits in the entry rows' spare upper halves
 constexpr int FT_TABLE = 256 * 256;
@@ -507,6 +507,9 @@ bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uin
   auto go = [&](auto kern, int waves) {
     hipLaunchKernelGGL(kern, grid, dim3(64 * waves), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc);
   };
+#ifndef BNB_LAB
+  if (g_fewtok_mode >= 16) return false;                    // (the ablation kernels exist in the lab build only)
+#else
   if (g_fewtok_mode >= 16) {                                // lab ablations: nested, <= 8 tokens, 48-row workgroups
     if (!nested || n > 8 || !s4) return false;
     constexpr bool X8L = true;
@@ -535,6 +538,7 @@ bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uin
     }
     return true;
   }
+#endif
   const bool x8 = n <= 8;
   auto by_rg = [&](auto mt_tag, auto nested_tag, auto s4_tag) {
     constexpr int MT = decltype(mt_tag)::value;
@@ -582,13 +586,22 @@ template bool launch_gemm_4bit_fewtok<fp16_t>(int, int, int, const fp16_t*, int,
 }  // namespace bnb
 
 extern "C" {
-// [lab, not in the header] timeline buffer of the ABL-128 variants (mode 16 + 128): 8 stamps per wave
+#ifdef BNB_LAB
+// [lab build only, not in the header] timeline buffer of the ABL-128 variants (mode 16 + 128): 8 stamps per wave
 int cgemm_4bit_fewtok_timeline(unsigned long long* buf) {
   BNB_RANGE("cgemm_4bit_fewtok_timeline");
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_ft_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
-// [additive, testing] whole-K few-token kernel: 0 = auto, 1 = off, 2 = wherever it fits
-void cgemm_4bit_set_fewtok_mode(int mode) { bnb::g_fewtok_mode = mode; }
+#endif
+// [additive, testing] whole-K few-token kernel: 0 = auto, 1 = off, 2 = wherever it fits (other values: auto; the lab
+// build also takes its ablation modes >= 16)
+void cgemm_4bit_set_fewtok_mode(int mode) {
+#ifdef BNB_LAB
+  bnb::g_fewtok_mode = mode;
+#else
+  bnb::g_fewtok_mode = (mode == 1 || mode == 2) ? mode : 0;
+#endif
+}
 // [additive] 1 when the 4-bit GEMM entry points run the whole-K few-token kernel for out features m, n activation rows,
 // in features k and this blocksize (the auto rule above, or the forced mode), else 0 -- the Python layer asks before
 // it sends 2..4 rows to the multi-row GEMV

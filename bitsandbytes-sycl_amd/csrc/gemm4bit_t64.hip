@@ -886,6 +886,7 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
     hipLaunchKernelGGL(kern, grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc, ws,
                        geo.ksplit, geo.kc, tickets, pstore);
   };
+#ifdef BNB_LAB
   if (g_t64_mode >= 16 && nested) {                          // lab ablations (nested bf16 / fp16 only)
     switch (g_t64_mode - 16) {
       case 1: lab(k_gemm_4bit_t64<T, true, 1>); break;
@@ -905,7 +906,11 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
       case 30 + 32 + 64 + 128 + 256: lab(k_gemm_4bit_t64<T, true, 30 + 32 + 64 + 128 + 256>); break;
       default: lab(k_gemm_4bit_t64<T, true>); break;
     }
-  } else if (g_t64_kp == 2 || (g_t64_kp == 0 && (n <= 48 || geo.ksplit == 1))) {
+  } else
+#else
+  (void)lab;
+#endif
+  if (g_t64_kp == 2 || (g_t64_kp == 0 && (n <= 48 || geo.ksplit == 1))) {
     if (nested)
       hipLaunchKernelGGL((k_gemm_4bit_t64<T, true, 0, 2>), grid, dim3(2 * T64_THREADS), 0, current_stream(), m, n, k, A,
                          lda, B, ldb, st, code, out, ldc, ws, geo.ksplit, geo.kc, tickets, pstore);
@@ -931,9 +936,10 @@ template bool launch_gemm_4bit_t64<fp16_t>(int, int, int, const fp16_t*, int, co
 }  // namespace bnb
 
 extern "C" {
-// [additive, testing] the 33..64-token kernel (gemm4bit_t64.hip): 0 = auto, 1 = off, 2 = wherever it applies (1..64
-// tokens); returns the previous setting
-int cgemm_4bit_set_t64_splits(int ks) {                   // [lab] force the split count (0 = the rule)
+// [additive, testing] the 33..64-token kernel's split-K count: ks > 0 forces it (tests of the combine and of ragged
+// splits; same results within the GEMM tolerance, bit-identical across the combine forms), 0 = the rule; returns the
+// previous setting
+int cgemm_4bit_set_t64_splits(int ks) {
   const int prev = bnb::g_t64_ks;
   bnb::g_t64_ks = ks;
   return prev;
@@ -954,10 +960,12 @@ int cgemm_4bit_set_t64_waves(int kp) {
   bnb::g_t64_kp = kp == 2 ? 2 : kp == 1 ? 1 : 0;
   return prev;
 }
-// [lab, not in the header] timeline buffer of the ABL-512 variant (mode 16 + 512): 8 stamps per wave
+#ifdef BNB_LAB
+// [lab build only, not in the header] timeline buffer of the ABL-512 variant (mode 16 + 512): 8 stamps per wave
 int cgemm_4bit_t64_timeline(unsigned long long* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_t64_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
+#endif
 // [additive, testing] the register-fed 33..64-token form: 0 = auto, 1 = off, 2 = wherever the kernel applies; returns the
 // previous setting
 int cgemm_4bit_set_t64_regfed(int v) {
@@ -970,10 +978,16 @@ int cgemm_4bit_set_t64_combine(int on) {
   bnb::g_t64_combine = on ? 1 : 0;
   return prev;
 }
+// [additive, testing] the 33..64-token kernel (gemm4bit_t64.hip): 0 = auto, 1 = off, 2 = wherever it applies (1..64
+// tokens; other values: auto -- the lab build also takes its ablation modes >= 15); returns the previous setting
 int cgemm_4bit_set_t64_mode(int mode) {
   BNB_RANGE("cgemm_4bit_set_t64_mode");
   const int prev = bnb::g_t64_mode;
+#ifdef BNB_LAB
   bnb::g_t64_mode = mode;
+#else
+  bnb::g_t64_mode = (mode == 1 || mode == 2) ? mode : 0;
+#endif
   return prev;
 }
 }

@@ -772,7 +772,9 @@ void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
 // [additive, testing] 1 = the wide GEMV one row per workgroup (the round-2 form); 0 = rows per workgroup by the rule
 void cgemv_4bit_set_wide_rows(int mode) { bnb::g_gemv_wide_rows = mode; }
 // [lab, not in the header] LDS bytes up to which the balanced GEMV runs two workgroups per CU (default 80 KiB)
-void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size_t)bytes; }
+#ifdef BNB_LAB
+void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size_t)bytes; }   // [lab build only]
+#endif
 // [additive, testing] nested statistics of the balanced GEMV decoded where each chunk is consumed (1) or all before the
 // first dot (0, default: measured faster); bit-identical; returns the previous setting
 int cgemv_4bit_set_lazy_nested(int on) {

@@ -25,6 +25,8 @@
 #include "int8_common.hpp"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <type_traits>
 #include <utility>
 
@@ -38,7 +40,7 @@ constexpr int HG_LDS_MAIN = 2 * HG_STAGE;         // 128 KiB
 // fragment writes of 16 consecutive rows then hit 2 banks each, 2-way at most)
 constexpr int HG_EPI_PITCH = 272;
 constexpr int HG_LDS_EPI = 4 * 128 * HG_EPI_PITCH;   // 136 KiB
-constexpr int HG_LDS = HG_LDS_MAIN > HG_LDS_EPI ? HG_LDS_MAIN : HG_LDS_EPI;
+[[maybe_unused]] constexpr int HG_LDS = HG_LDS_MAIN > HG_LDS_EPI ? HG_LDS_MAIN : HG_LDS_EPI;
 
 // LDS-DMA with a scalar base: lane address = sbase + voff (unsigned 32-bit), 16 B per lane to lds + 16 * lane.
 // M0 (the LDS destination) is written and restored inside the statement (it is compiler-reserved).
@@ -169,7 +171,8 @@ __device__ __forceinline__ uint32_t mm_dequant_pair(int32_t a0, int32_t a1, floa
 // Round 4: the three-barrier operand-split schedule (V & 8192, tile3 below) is the launched one: bit-identical to the
 // two-half schedule and 0.8-1.5 % faster at 4096 x 4096 x 11008 (bf16 234.6-235.3 vs 236.6-238.6 us; int8 4-wave
 // 127.3-129.3 vs 128.7-129.3 us; tools/hgemm_variant_ab.py, profiles/lab/r04_hgemm_variants.txt).  The round-3
-// two-half schedule stays selectable at run time (chgemm_set_variant(1)) as the A/B arm.
+// two-half schedule is no longer launched (round 6): its compiled loop carried accumulator copies between the asm MFMAs
+// (the note "The round-3 two-half schedule ..." below); the code stays for tools/hgemm_lab.hip.
 constexpr int HG_V = 16 + 8192;
 // variant bit: the full-tile 16-bit epilogue stores C write-through (sc1), so the launch ends with no dirty L2 lines for
 // the next kernel's boundary to write back (chgemm_set_c_store; on by default: int8 igemmlt+dequant at the metric shape
@@ -183,7 +186,7 @@ static int g_hg_cwt = 1;
 constexpr int HG_V_EPI = 65536;
 static int g_hg_epi = 1;
 // variant bit (with HG_V_EPI only): the interleaved epilogue's C stores carry the non-temporal hint (nt), so the output
-// (not re-read by this step) does not displace the operands in the last-level cache (chgemm_set_c_store(2 / 3); lab)
+// (not re-read by this step) does not displace the operands in the last-level cache (chgemm_set_c_store(2); A/B arm)
 constexpr int HG_V_CNT = 131072;
 // variant bit (lab): per-wave s_memrealtime stamps (10 ns ticks) at g_hg_tl[(blockIdx.x * 4 + wave) * 8 + i]: kernel
 // start, prologue done (tile 0 landed, first barrier), k-loop done (DMA drained), epilogue's stores issued, stores
@@ -192,14 +195,22 @@ constexpr int HG_V_TL = 262144;
 __device__ unsigned long long* g_hg_tl = nullptr;
 __device__ int g_hg_tl_nswap = 0;      // lab, HG_V_TL only: 1 = each XCD takes the other half of the N-tiles
 __device__ int g_hg_tl_nostore = 0;    // lab, HG_V_TL only: 1 = the interleaved epilogue's C stores are dropped
-static int g_hg_tl_on = 0;
+[[maybe_unused]] static int g_hg_tl_on = 0;     // (lab build: chgemm_timeline)
 __device__ __forceinline__ unsigned long long hg_now() {
   unsigned long long t;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   return t;
 }
-constexpr int HG_V_ALT = 8 + 16 + 4096;
-static int g_hgemm_variant = 0;
+// The round-3 two-half schedule (V = 8 + 16 + 4096) was the run-time A/B arm chgemm_set_variant(1) until round 6, when
+// the cause of its int8 non-determinism (round 5, profiles/lab/r05_diag_int8_variant.txt) was found in the ISA, not in
+// the waits: hipcc's register allocator, which sees an asm MFMA as an opaque statement, rotated accumulators through the
+// two-half loop with v_accvgpr_read / v_accvgpr_mov (192-208 of them between the MFMAs of the V = 4120 kernels, e.g.
+// `v_accvgpr_read_b32 v167, a55` six MFMAs after the asm MFMA that writes a[52:55]), without the MFMA -> AGPR-read wait
+// states that its hazard recognizer inserts only for MFMAs it knows -- so a copy could read an accumulator before the
+// MFMA wrote it, and which value it read depended on timing (only element 0 of acc[3][*] in the int8 kernel: one copied
+// register of the rotation).  The bf16 / fp16 arms carried the same copies and passed by timing alone.  The arm is
+// gone; tests/test_kernel_resources.py now checks that no k_hgemm kernel has an accumulator read, write or move between
+// its first and last MFMA.
 // lda / ldb / ldc in elements of the operand / output type.  rowStats / colStats / bias: HG_I8_DEQ only.
 // SPLIT (bf16 / fp16 only): the split-K form -- its epilogue stores fp32 partials only.  A separate instantiation, so
 // that each kernel has ONE epilogue reading the accumulators (two in one kernel made the allocator spill).
@@ -312,11 +323,121 @@ struct HgSide {
   void* out;                 // ndw * 8 outputs of the GEMM's type (16-B aligned)
   long long ndw;             // packed dwords (elements / 8)
   int per_wg, iters, every, bs_shift, bs2_shift, nested, fp4;
-  int mode;                  // A/B bits (chgemm_set_side_mode): 1 = non-temporal packed loads / output stores; lab
-                             // ablations (timing only, wrong weights): 2 = no side stores, 8 = no consumption, 16 = no
-                             // side loads, 32 = no side step in the loop, 64 = no tail
+  int mode;                  // A/B bits (chgemm_set_side_mode): 1 = non-temporal packed loads / output stores; 128 =
+                             // the round-4 in-loop form instead of the tail form (below); lab ablations (timing only,
+                             // wrong weights): 2 = no side stores, 8 = no consumption, 16 = no side loads, 32 = no side
+                             // step in the loop, 64 = no tail
+  uint32_t* ticket;          // tail form: the launch's chunk counter + finished-workgroup counter (nullptr: static)
 };
 static int g_side_mode = 1;
+
+// Tail form of the side dequantise (round 6, V & HG_V_TAIL, the default of chgemm_tn_pf_*): no side work inside the
+// k-loop at all -- each workgroup, once its tile's epilogue has issued its C stores, dequantises chunks of the next
+// weight, taken first by its own index and then from a shared counter (work stealing) until none is left.  Why: the
+// k-loop ends up to ~8 % apart between the fastest and the slowest XCD on identical work (DESIGN.md §5 'Where k_hgemm's
+// fixed time goes': the same physical XCDs are slow in every shape and run), so with one tile per CU the fast XCDs idle
+// while the slow ones finish; here they spend that time on the next weight, and the next call runs its GEMM alone.
+// The in-loop form (round 4) paid for its side work in MFMA issue slots (+50 us at the metric shape); the tail form
+// takes no issue slot from any MFMA.  Values: exactly k_dequantize_4bit_stream's (code * absmax in fp32, one RNE cast;
+// nested: code2[q8] * absmax2 + offset) -- the same helper arithmetic as the in-loop form, whatever workgroup does a
+// chunk.  The counter pair is per stream (host: hg_tail_ticket) and reset by the last workgroup to finish, so the next
+// launch on that stream finds it at zero; under HIP-graph capture the launch takes the static assignment (chunk c to
+// workgroup c mod grid) instead, with no counter.
+constexpr int HG_V_TAIL = 524288;
+constexpr int HG_TAIL_U = 8;                               // 4-dword lane groups per wave chunk (256 dwords each)
+
+// one wave's chunk c: HG_TAIL_U groups of 256 packed dwords (4 per lane, 32 weights, one statistics block); the loads
+// of a chunk land in w / am, hg_tail_store converts and stores them
+struct HgTailRegs {
+  hg_u32x4_t w[HG_TAIL_U];
+  float am[HG_TAIL_U];
+};
+__device__ __forceinline__ void hg_tail_load(const HgSide& side, const float* s_c2, float off, uint32_t c, int lane,
+                                             HgTailRegs& r) {
+  const uint32_t base = c * (256u * HG_TAIL_U);
+#pragma unroll
+  for (int u = 0; u < HG_TAIL_U; ++u) {
+    const uint32_t gd = min(base + 256u * u + 4u * (uint32_t)lane, (uint32_t)side.ndw - 4u);
+    r.w[u] = __builtin_nontemporal_load(reinterpret_cast<const hg_u32x4_t*>(side.packed + 4ull * gd));
+    const uint32_t blk = (gd * 8u) >> side.bs_shift;
+    r.am[u] = side.nested ? __fadd_rn(__fmul_rn(s_c2[side.q8[blk]], side.absmax2[blk >> side.bs2_shift]), off)
+                          : side.absmax[blk];
+  }
+}
+template <typename T16>
+__device__ __forceinline__ void hg_tail_store(const HgSide& side, const float2* s_pair, uint32_t c, int lane,
+                                              const HgTailRegs& r) {
+  const uint32_t base = c * (256u * HG_TAIL_U);
+#pragma unroll
+  for (int u = 0; u < HG_TAIL_U; ++u) {
+    const uint32_t gd = base + 256u * u + 4u * (uint32_t)lane;
+    if (gd >= (uint32_t)side.ndw) continue;               // (ndw % 4 == 0: a lane's 4 dwords are all in or all out)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hg_u32x4_t o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 p = s_pair[(r.w[u][j] >> (8 * i)) & 0xFF];
+        o[i] = cvt_pk<T16>(__fmul_rn(p.x, r.am[u]), __fmul_rn(p.y, r.am[u]));
+      }
+      // device-scope write-through (sc1), as k_dequantize_4bit_stream's default store policy: the next launch reads it
+      asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" : : "v"((gd + (uint32_t)j) * 16u), "v"(o),
+                   "s"(side.out) : "memory");
+    }
+  }
+}
+
+// The tail form's loop, run by every wave on its own after the epilogue: no workgroup barrier (a barrier's release
+// fence would wait for every store issued so far), the wave's own LDS copy of the code-pair table (2 KiB) and nested
+// code map (1 KiB) in its own epilogue staging rows (`ep`, which it has finished reading: LDS operations of one wave
+// run in order), its first chunk by its wave index and the rest from the counter, and each chunk's loads issued before
+// the previous chunk is converted and stored (two register sets).
+template <typename T16>
+__device__ __forceinline__ void hg_side_tail(const HgSide& side, uint8_t* ep, int lane, uint32_t wave_id,
+                                             uint32_t waves) {
+  float2* s_pair = reinterpret_cast<float2*>(ep);
+  float* s_c2 = reinterpret_cast<float*>(ep + 2048);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = lane + 64 * q;
+    s_pair[e] = side.fp4 ? make_float2(code4_value<FP4>(e >> 4), code4_value<FP4>(e & 15))
+                         : make_float2(code4_value<NF4>(e >> 4), code4_value<NF4>(e & 15));
+    if (side.nested) s_c2[e] = side.code2[e];
+  }
+  const float off = side.nested ? *side.offset : 0.0f;
+  const uint32_t nchunks = (uint32_t)((side.ndw + 256 * HG_TAIL_U - 1) / (256 * HG_TAIL_U));
+  auto take = [&](uint32_t cur) -> uint32_t {             // the chunk after `cur` for this wave
+    if (side.ticket == nullptr) return cur + waves;
+    uint32_t t = 0;
+    if (lane == 0) t = waves + atomicAdd(side.ticket, 1u);
+    return __builtin_amdgcn_readfirstlane(t);
+  };
+  HgTailRegs r0, r1;
+  uint32_t c = wave_id;
+  if (c < nchunks) {
+    hg_tail_load(side, s_c2, off, c, lane, r0);
+    while (true) {
+      const uint32_t n = take(c);
+      if (n < nchunks) hg_tail_load(side, s_c2, off, n, lane, r1);
+      hg_tail_store<T16>(side, s_pair, c, lane, r0);
+      if (n >= nchunks) break;
+      c = n;
+      const uint32_t n2 = take(c);
+      if (n2 < nchunks) hg_tail_load(side, s_c2, off, n2, lane, r0);
+      hg_tail_store<T16>(side, s_pair, c, lane, r1);
+      if (n2 >= nchunks) break;
+      c = n2;
+    }
+  }
+  if (side.ticket != nullptr && lane == 0) {
+    // the last wave to get here (every other one has taken its final chunk number) resets the pair for the next launch
+    // on this stream
+    if (atomicAdd(side.ticket + 1, 1u) == waves - 1) {
+      atomicExch(side.ticket, 0u);
+      atomicExch(side.ticket + 1, 0u);
+    }
+  }
+}
 
 template <int OP, int V = 0, bool SPLIT = false, int WI = 8, int WJ = 8, bool SIDE = false>
 __global__ void __launch_bounds__(HG_THREADS, 1)
@@ -1023,6 +1144,14 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
     }
   }
   (void)value;
+  if constexpr ((V & HG_V_TAIL) != 0) {
+    // (a bare s_barrier, no fence: every wave is past its last LDS read -- the last k-tile's fragments fed its MFMAs,
+    // its staging rows fed its stores -- before any wave writes its table over stage / staging bytes; a __syncthreads
+    // release fence would also wait for the C stores)
+    __builtin_amdgcn_s_barrier();
+    hg_side_tail<T16>(side, smem + wave * (16 * WI * EPI_PITCH), lane_e, blockIdx.x * 4u + (uint32_t)wave,
+                      gridDim.x * 4u);
+  }
   if constexpr (TL) {
     const unsigned long long tl3 = hg_now();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1129,10 +1258,54 @@ static void hgemm_launch_side(const HgPlan& pl, int m, int n, int k, const void*
   }
 }
 
+// The tail form's chunk counter pair for launches on the current stream of the current device (zeroed once; each launch's
+// last workgroup resets it).  Launches on one stream run one after another, so a pair is never shared by two launches
+// at once.  nullptr under HIP-graph capture (a captured launch would bake the pair in, and its replays could run beside
+// eager launches on the stream it was captured from) or when the allocation fails: the static chunk assignment then.
+static uint32_t* hg_tail_ticket() {
+  hipStream_t st = current_stream();
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, uint32_t*> pairs;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(dev, st);
+  const auto it = pairs.find(key);
+  if (it != pairs.end()) return it->second;
+  void* p = nullptr;
+  if (hipMalloc(&p, 2 * sizeof(uint32_t)) != hipSuccess || hipMemsetAsync(p, 0, 2 * sizeof(uint32_t), st) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  pairs[key] = static_cast<uint32_t*>(p);
+  return static_cast<uint32_t*>(p);
+}
+
+// false: a side dequantise was asked for that this kind / shape does not run (nothing launched)
 template <int OP, int V, int WI, int WJ>
-static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
+static bool hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
                                long long ldb, void* C, long long ldc, const float* rowStats, const float* colStats,
                                const fp16_t* bias, float* ws, const HgSide* side) {
+  // the tail form (default, round 6): the launched 16-bit kind, every tile shape; chgemm_set_side_mode(128 | ...) keeps
+  // the round-4 in-loop form below
+  if constexpr ((OP == HG_BF16 || OP == HG_FP16) && V == (HG_V | HG_V_CWT | HG_V_EPI)) {
+    if (side && !(g_side_mode & 128)) {
+      HgSide sd = *side;
+      sd.mode = g_side_mode;
+      sd.ticket = hg_tail_ticket();
+      hgemm_launch_side<OP, V | HG_V_TAIL, WI, WJ, false>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
+                                                          ws, sd);
+      return true;
+    }
+  }
   if constexpr ((OP == HG_BF16 || OP == HG_FP16) && (V & 8192) != 0 && !(WI == 4 && WJ == 4)) {
     if (side) {
       const long long wgs = (long long)((m + 32 * WI - 1) / (32 * WI)) * ((n + 32 * WJ - 1) / (32 * WJ)) * pl.splits;
@@ -1147,10 +1320,12 @@ static void hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void
       // (the side form keeps the round-4 epilogue: with the side's state live the interleaved one spills)
       hgemm_launch_side<OP, (V & ~(HG_V_EPI | HG_V_CNT | HG_V_TL)), WI, WJ, true>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
                                                            ws, sd);
-      return;
+      return true;
     }
   }
+  if (side) return false;           // (never launch the GEMM without the side dequantise the caller counts on)
   hgemm_launch_side<OP, V, WI, WJ, false>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, HgSide{});
+  return true;
 }
 
 template <int OP>
@@ -1161,17 +1336,12 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   // the dequant epilogue reads 4 column scales / 4 bias halves per 16-B / 8-B load
   if (OP == HG_I8_DEQ && (((uintptr_t)colStats & 15) || ((uintptr_t)bias & 7))) return 1;
   constexpr bool FP = OP == HG_BF16 || OP == HG_FP16;
-  // The round-3 schedule arm (chgemm_set_variant(1)) is an A/B arm of the 16-bit kinds only: on the int8 body it is
-  // not deterministic (round 5, tools/r05_diag_int8_variant.py: ~65 k of 16.8 M outputs differ run to run at 4096 x
-  // 4096 x 11008, whole 8-row DMA pieces -- a stage read racing a piece of the two-half schedule; the launched
-  // three-barrier schedule is deterministic and equal to the 8-wave igemm_256 bit for bit), so int8 always runs the
-  // default schedule.
-  const int variant = FP ? g_hgemm_variant : 0;
-  // int8 (HG_I8_DEQ) and the round-3 schedule arm run the 256 x 256 tile only
-  const bool full_only = !FP || variant == 1;
-  if (side && (!FP || variant == 1)) return 1;
-  // (the 128 x 128 tile: 16-bit kinds without a side dequantise -- the side form is not built for it)
-  const bool quarter = FP && side == nullptr;
+  // int8 (HG_I8_DEQ) runs the 256 x 256 tile only
+  const bool full_only = !FP;
+  if (side && !FP) return 1;
+  // (the 128 x 128 tile: 16-bit kinds without a side dequantise or with its tail form -- the in-loop form is not built
+  // for it)
+  const bool quarter = FP && (side == nullptr || (!(g_side_mode & 128) && g_hg_cwt == 1 && g_hg_epi));
   HgPlan pl = hgemm_plan(m, n, k, HgOpT<OP>::ELEM, FP, full_only, quarter);
   if (pl.splits > 1 && (ws == nullptr || ((uintptr_t)ws & 15) ||
                         ws_bytes < (long long)pl.splits * m * n * (long long)sizeof(float)))
@@ -1180,30 +1350,34 @@ int hgemm_launch(int m, int n, int k, const void* A, long long lda, const void* 
   auto by_shape = [&](auto vtag) {
     constexpr int VV = decltype(vtag)::value;
     if (pl.wi == 8 && pl.wj == 8)
-      hgemm_launch_shape<OP, VV, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-    else if constexpr (FP) {
-      if (pl.wi == 8) hgemm_launch_shape<OP, VV, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-      else if (pl.wj == 8) hgemm_launch_shape<OP, VV, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
-      else hgemm_launch_shape<OP, VV, 4, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
+      return hgemm_launch_shape<OP, VV, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+    if constexpr (FP) {
+      if (pl.wi == 8) return hgemm_launch_shape<OP, VV, 8, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+      if (pl.wj == 8) return hgemm_launch_shape<OP, VV, 4, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
+      return hgemm_launch_shape<OP, VV, 4, 4>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, side);
     }
+    return false;
   };
-  if (variant == 1) {
-    hgemm_launch_shape<OP, HG_V_ALT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias, ws, nullptr);
-  } else if (FP && g_hg_tl_on && g_hg_cwt == 1 && g_hg_epi && pl.wi == 8 && pl.wj == 8 && !side) {   // lab timeline
+  bool launched = true;
+#ifdef BNB_LAB
+  if (FP && g_hg_tl_on && g_hg_cwt == 1 && g_hg_epi && pl.wi == 8 && pl.wj == 8 && !side) {   // lab timeline
     // (16-bit kinds only: on the int8 body the stamps' registers spilled)
     if constexpr (FP)
-      hgemm_launch_shape<OP, HG_V | HG_V_CWT | HG_V_EPI | HG_V_TL, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats,
-                                                                       colStats, bias, ws, nullptr);
-  } else if (g_hg_cwt == 2 && g_hg_epi && pl.wi == 8 && pl.wj == 8) {   // the lab's nt arm: full tile only
-    hgemm_launch_shape<OP, HG_V | HG_V_CWT | HG_V_EPI | HG_V_CNT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats,
-                                                                      colStats, bias, ws, side);
+      launched = hgemm_launch_shape<OP, HG_V | HG_V_CWT | HG_V_EPI | HG_V_TL, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc,
+                                                                                  rowStats, colStats, bias, ws, nullptr);
+  } else
+#endif
+  if (g_hg_cwt == 2 && g_hg_epi && pl.wi == 8 && pl.wj == 8) {   // the lab's nt arm: full tile only
+    launched = hgemm_launch_shape<OP, HG_V | HG_V_CWT | HG_V_EPI | HG_V_CNT, 8, 8>(pl, m, n, k, A, lda, B, ldb, C, ldc,
+                                                                                 rowStats, colStats, bias, ws, side);
   } else if (g_hg_cwt && g_hg_epi) {
-    by_shape(std::integral_constant<int, HG_V | HG_V_CWT | HG_V_EPI>{});
+    launched = by_shape(std::integral_constant<int, HG_V | HG_V_CWT | HG_V_EPI>{});
   } else if (g_hg_cwt) {
-    by_shape(std::integral_constant<int, HG_V | HG_V_CWT>{});
+    launched = by_shape(std::integral_constant<int, HG_V | HG_V_CWT>{});
   } else {
-    by_shape(std::integral_constant<int, HG_V>{});
+    launched = by_shape(std::integral_constant<int, HG_V>{});
   }
+  if (!launched) return 1;          // (a side dequantise this kind / shape does not run: nothing launched)
   if constexpr (FP) {
     using T = typename std::conditional<OP == HG_BF16, bf16_t, fp16_t>::type;
     if (pl.splits > 1) launch_splitk_rows_reduce<T>(ws, pl.splits, m, n, reinterpret_cast<T*>(C), (int)ldc);
@@ -1305,7 +1479,7 @@ long long chgemm_tn_workspace_bytes(int m, int n, int k) { return bnb::hgemm_wor
 // k-tiles per split}; the output tile is 32 WI x 32 WJ (256 x 256, 256 x 128 or 128 x 256)
 void chgemm_tn_plan(int m, int n, int k, int* out) {
   BNB_RANGE("chgemm_tn_plan");
-  const bnb::HgPlan pl = bnb::hgemm_plan(m, n, k, 2, true, bnb::g_hgemm_variant == 1, true);
+  const bnb::HgPlan pl = bnb::hgemm_plan(m, n, k, 2, true, false, true);
   out[0] = pl.wi;
   out[1] = pl.wj;
   out[2] = pl.splits;
@@ -1328,7 +1502,9 @@ int chgemm_set_quarter_tile(int mode, int kt_x1000) {
   if (kt_x1000 > 0) bnb::g_hg_quarter_kt = kt_x1000 / 1000.0;
   return prev;
 }
-// [lab, not in the header] per-wave timeline of the 256 x 256 k_hgemm (HG_V_TL): buf = 8 u64 per wave (nullptr: off)
+#ifdef BNB_LAB
+// [lab build only (make lab), not in the header] per-wave timeline of the 256 x 256 k_hgemm (HG_V_TL): buf = 8 u64 per
+// wave (nullptr: off); _nswap / _nostore: the XCD N-tile swap and the dropped-store ablation (wrong results: lab only)
 int chgemm_timeline_nswap(int v) {
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_hg_tl_nswap), &v, sizeof(v)) == hipSuccess ? 0 : 1;
 }
@@ -1339,6 +1515,7 @@ int chgemm_timeline(unsigned long long* buf) {
   bnb::g_hg_tl_on = buf != nullptr;
   return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_hg_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
 }
+#endif
 // [additive, testing] 1 (default): the interleaved 16-bit epilogue (HG_V_EPI, with write-through C), 0: the round-4 one
 // (convert and stage everything, then store); returns the previous setting
 int chgemm_set_epilogue(int v) {
@@ -1346,17 +1523,16 @@ int chgemm_set_epilogue(int v) {
   bnb::g_hg_epi = v ? 1 : 0;
   return prev;
 }
+// [additive, testing] the side dequantise's load / store hint: bit 1 = non-temporal (default); the lab build also takes
+// its ablation bits (2 / 8 / 16 / 32 / 64: wrong weights, timing only), the product library masks them off
 int chgemm_set_side_mode(int v) {
   BNB_RANGE("chgemm_set_side_mode");
   const int prev = bnb::g_side_mode;
+#ifdef BNB_LAB
   bnb::g_side_mode = v;
-  return prev;
-}
-// [additive, testing] k_hgemm schedule: 0 = the default, 1 = the A/B arm (HG_V_ALT); returns the previous setting
-int chgemm_set_variant(int v) {
-  BNB_RANGE("chgemm_set_variant");
-  const int prev = bnb::g_hgemm_variant;
-  bnb::g_hgemm_variant = v;
+#else
+  bnb::g_side_mode = v & (1 | 128);
+#endif
   return prev;
 }
 

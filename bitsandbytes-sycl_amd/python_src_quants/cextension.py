@@ -53,7 +53,7 @@ class BNBNativeLibrary:
                      "cint8_row_quant_fp16", "cgemm_4bit_inference_nested_ws_bf16",
                      "cgemm_4bit_inference_nested_ws_fp16", "cset_cpu_threads", "cgemm_4bit_fewtok_takes", "chgemm_tn_ws_bf16", "chgemm_tn_ws_fp16",
                      "cipc_handle_size", "cipc_get_handle", "cipc_open_handle", "cipc_close_handle", "callgather_ipc_16",
-                     "chgemm_set_variant", "cprobe_lds_poison", "cprobe_lds_peek", "croctx_enabled"):
+                     "cprobe_lds_poison", "cprobe_lds_peek", "croctx_enabled"):
             getattr(lib, name).restype = ct.c_int
 
     def __getattr__(self, item):

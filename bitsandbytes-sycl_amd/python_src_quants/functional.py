@@ -973,7 +973,10 @@ def _tuned_route(A2: Tensor, Bc: Tensor, state: QuantState, out: Tensor, absmax:
         ws_key = (A2.device, A2.dtype, _stream_key(A2.device))
         ws_before = _DEQ_WS.get(ws_key)
         rows, N, K = A2.shape[0], state.shape[0], state.shape[1]
-        names = [n for n in GEMM_4BIT_ROUTES if n != "hgemm" or _hgemm_fits(rows, N, K)]
+        # "hgemm" is always a candidate (gemm_4bit runs it in row / weight chunks beyond one launch's offsets); the
+        # library candidates dequantise the whole weight with a 32-bit element count, so not from 2^31 elements on
+        big = N * K >= 2 ** 31
+        names = [n for n in GEMM_4BIT_ROUTES if not (big and n in ("library", "library_tn"))]
         for name in names:      # untimed: code-object loads, the rocBLAS solution search, workspaces, clock ramp
             gemm_4bit(A2, Bc, state, out=out, absmax=absmax, _route=name)
         times = {name: float("inf") for name in names}
@@ -1138,9 +1141,10 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
               _route: Optional[str] = None, prefetch: Optional[tuple] = None) -> Tensor:
     """4-bit weight GEMM for any number of activation rows (the M>1 slot of cgemm_4bit_inference,
     ref:pythonInterface.cpp:377).  out[..., n] = A[..., :] @ W^T with W the dequantised [N, K] weight;
-    replaces dequantize_4bit + F.linear (autograd/_functions.py:507).  Large problems (see
-    GEMM_4BIT_DEQUANT_MIN_ROWS): the HIP dequantise kernel into a weight workspace + one hipBLASLt GEMM;
-    otherwise the fused kernel (dequantise in LDS + MFMA, split-K when the tile grid is small).
+    replaces dequantize_4bit + F.linear (autograd/_functions.py:507).  The route per shape is
+    gemm_4bit_static_route: from 65 rows (outside the fused-kernel band) the HIP dequantise kernel into a weight
+    workspace + the hand-written k_hgemm (hgemm.hip; chunked beyond one launch's 32-bit offsets), otherwise the
+    few-token kernels or the fused kernel (dequantise in LDS + MFMA, split-K when the tile grid is small).
     B is the packed uint8 weight (any view of the N*K/2 bytes).  events (bench instrumentation): a list
     that receives (name, start, end) torch.cuda.Event pairs around the launched stages.  reuse_weight:
     the caller runs several row chunks of one product against the same, unmodified weight (the chunked
@@ -1179,8 +1183,16 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, out: Optional[Tensor] = N
             route = measured
     if route == "hgemm" and not _hgemm_fits(rows, N, K):
         # beyond one launch's 32-bit offsets: the same pair in row / weight chunks (also where a measured / imported
-        # route, which covers a quarter-octave of row counts, names "hgemm" near the limit)
-        return _gemm_4bit_hgemm_chunked(A2, Bc, state, out, absmax).view(*A.shape[:-1], N)
+        # route, which covers a quarter-octave of row counts, names "hgemm" near the limit).  reuse_weight and prefetch
+        # do not apply there (each call dequantises its weight chunk by chunk); events get one "gemm" pair around it all
+        ev = _stage_events(2) if events is not None else None
+        if ev:
+            ev[0].record()
+        _gemm_4bit_hgemm_chunked(A2, Bc, state, out, absmax)
+        if ev:
+            ev[1].record()
+            events.append(("gemm", ev[0], ev[1]))
+        return out.view(*A.shape[:-1], N)
     library = route in ("library", "library_tn", "hgemm")
     if (not library and 2 <= rows <= GEMM_4BIT_GEMV_TOKENS and not _fewtok_takes(N, rows, K, state.blocksize)
             and _gemm_4bit_tokens(A2, Bc, state, out, absmax, events)):

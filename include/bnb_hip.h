@@ -255,6 +255,13 @@ int chgemm_tn_pf_fp16(int m, int n, int k, const bnb_fp16* A, int lda, const bnb
 /* [additive, testing] the 33..64-token 4-bit GEMM kernel (gemm4bit_t64.hip): 0 = auto (33..64 activation rows,
  * blocksize 64, K % 256 == 0), 1 = off, 2 = wherever it applies (1..64 rows); returns the previous setting */
 int cgemm_4bit_set_t64_mode(int mode);
+/* [additive, testing] that kernel's split-K count: ks > 0 forces it (within the GEMM tolerance of the rule's split;
+ * the combine forms stay bit-identical to each other), 0 = the rule; returns the previous setting */
+int cgemm_4bit_set_t64_splits(int ks);
+/* [additive, testing] geometry of the split-K few-token kernel (gemm4bit_skinny.hip): -1 (default) = the rule, 0 = 4
+ * waves, 1 = 8 waves with the same blocks per split, 2 = 8 waves with twice the blocks per split; results within the
+ * GEMM tolerance */
+void cgemm_4bit_set_skinny_config(int cfg);
 /* [additive, testing] split-K combine of that kernel: 1 = by the last workgroup of each row tile to finish (device-scope
  * partials, vmcnt(0) + barrier, then a ticket; splits summed in order), 0 (default) = a separate reduce launch (faster:
  * DESIGN.md §4); returns the previous setting */
@@ -281,7 +288,8 @@ int cdequantize_set_store_policy(int policy);
  * scalar loads (1, where blocksize 64 / blocksize2 >= 64 / 64-B aligned codes allow) or per lane (0, default: measured
  * faster); bit-identical; returns the previous setting */
 int cdequantize_set_nested_scalar(int on);
-/* [additive, testing] k_hgemm side-dequantise A/B bits (chgemm_tn_pf_*); returns the previous value */
+/* [additive, testing] k_hgemm side dequantise (chgemm_tn_pf_*): bit 1 (default) = non-temporal side loads / stores,
+ * 0 = plain; other bits are ignored (the lab build's ablations); returns the previous value */
 int chgemm_set_side_mode(int v);
 /* [additive, testing] 1 (default): k_hgemm stores C and its split-K partials write-through (device scope), 0:
  * write-back, 2: write-through + non-temporal hint (256 x 256 tile, interleaved epilogue; others as 1); returns the
@@ -291,8 +299,6 @@ int chgemm_set_c_store(int wt);
  * (default), 2 = forced wherever allowed (no side dequantise); kt_x1000 > 0 sets the tile's k-tile time for the cost
  * model (256 x 256 k-tile units x 1000); returns the previous mode */
 int chgemm_set_quarter_tile(int mode, int kt_x1000);
-/* [additive, testing] k_hgemm schedule A/B knob: 0 = default, 1 = the alternative arm; returns the previous value */
-int chgemm_set_variant(int v);
 /* [additive, testing] k_hgemm's 16-bit epilogue: 1 (default) = interleaved per 16-row group (conversion overlapped with
  * the previous group's stores), 0 = the round-4 form; bit-identical outputs; returns the previous setting */
 int chgemm_set_epilogue(int v);

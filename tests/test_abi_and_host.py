@@ -31,6 +31,26 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
 
 
+def test_library_exports_nothing_outside_the_header():
+    """the product library's dynamic symbol table is exactly the header's functions (linker version
+    script generated from include/bnb_hip.h, csrc/Makefile) -- no lab hook (per-wave timelines, ablation modes that drop
+    work) and no C++ internal is reachable through it; those live in the lab build (`make lab`)."""
+    import shutil
+    import subprocess
+    import python_src_quants as bnb
+    nm = shutil.which("nm")
+    if nm is None:
+        pytest.skip("no nm")
+    path = str(bnb.cextension.get_hip_bnb_library_path())
+    out = subprocess.run([nm, "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if len(ln.split()) == 3 and ln.split()[1] in "TtWw"}
+    assert exported == set(_header_symbols()), (sorted(exported - set(_header_symbols())),
+                                                sorted(set(_header_symbols()) - exported))
+    for lab_only in ("chgemm_timeline", "chgemm_timeline_nostore", "cgemm_4bit_t64_timeline",
+                     "cgemm_4bit_fewtok_timeline", "chgemm_set_variant"):
+        assert lab_only not in exported
+
+
 def test_reference_abi_names_present():
     """The hot-path names of ref:sycl/pythonInterface.cpp:192-422 are all exported."""
     import python_src_quants as bnb

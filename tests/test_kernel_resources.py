@@ -147,3 +147,21 @@ def test_hgemm_tile3_dma_count_between_waits(hgemm_device_asm):
         side_seen |= side
     assert shapes_seen == set(plans), shapes_seen
     assert side_seen
+
+
+def test_hgemm_no_accumulator_copies_between_mfmas(hgemm_device_asm):
+    """k_hgemm issues its MFMAs from inline asm with the accumulators pinned to AGPRs ("+a").  hipcc cannot see that such
+    a statement is an MFMA, so it inserts no MFMA -> AGPR-read wait states: any v_accvgpr_read / _write / _mov the
+    register allocator places between two asm MFMAs may read an accumulator before the MFMA wrote it.  That is what made
+    the removed round-3 schedule arm non-deterministic on int8 (192-208 such copies in its loop).  Every
+    k_hgemm kernel built into the library must hold none between its first and last MFMA (the epilogue reads the
+    accumulators after the hand-written wait-state pad that follows the last one)."""
+    text = hgemm_device_asm[0]
+    bodies = re.findall(r"^(_ZN3bnb7k_hgemm\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.S | re.M)
+    assert bodies, "no k_hgemm kernels"
+    for name, body in bodies:
+        lines = [ln.split(";")[0].strip() for ln in body.splitlines()]
+        mf = [i for i, ln in enumerate(lines) if ln.startswith("v_mfma")]
+        assert mf, name
+        copies = [ln for ln in lines[mf[0]:mf[-1]] if re.match(r"v_accvgpr_(read|write|mov)", ln)]
+        assert not copies, (name, len(copies), copies[:3])

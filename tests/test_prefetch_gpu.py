@@ -37,6 +37,7 @@ def _plain_gemm(X, W):
     wsb = int(lib.chgemm_tn_workspace_bytes(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K)))
     ws = F._gemm_workspace(X.device, wsb)
     fn = lib.chgemm_tn_ws_bf16 if X.dtype == torch.bfloat16 else lib.chgemm_tn_ws_fp16
+    F.post_call(F.pre_call(X.device))       # bind the library to torch's current stream (as gemm_4bit does)
     assert fn(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K), F.get_ptr(X), ct.c_int32(K), F.get_ptr(W), ct.c_int32(K),
               F.get_ptr(out), ct.c_int32(N), F.get_ptr(ws), ct.c_longlong(wsb)) == 0
     return out
@@ -51,9 +52,22 @@ def _pf_gemm(X, W, pf):
     target = torch.full((sn.shape[0] * sn.shape[1],), float("nan"), device="cuda", dtype=X.dtype)
     wsb = int(lib.chgemm_tn_workspace_bytes(ct.c_int32(rows), ct.c_int32(N), ct.c_int32(K)))
     ws = F._gemm_workspace(X.device, wsb)
+    F.post_call(F.pre_call(X.device))       # bind the library to torch's current stream (as gemm_4bit does)
     rc = F._launch_prefetch_gemm(X, W, out, ws, wsb, pf, target)
     assert rc == 0, rc
     return out, target.view(sn.shape[0], sn.shape[1])
+
+
+# the two side-dequantise forms: 1 = the tail form (default since round 6: after the tile's epilogue, chunks taken by
+# work stealing), 129 = the round-4 in-loop form (side steps between the MFMAs); both non-temporal side loads
+FORMS = [1, 129]
+
+
+@pytest.fixture(params=FORMS, ids=["tail", "inloop"])
+def side_form(request):
+    prev = lib.chgemm_set_side_mode(request.param)
+    yield request.param
+    lib.chgemm_set_side_mode(prev)
 
 
 # (rows, N, K) of the GEMM -> its launch plan (WI, WJ, splits)
@@ -67,7 +81,7 @@ GEMMS = [
 
 @pytest.mark.parametrize("gemm,plan", GEMMS, ids=[f"{g[0]}x{g[1]}x{g[2]}" for g, _ in GEMMS])
 @pytest.mark.parametrize("qt,nested", [("nf4", True), ("nf4", False), ("fp4", True), ("fp4", False)])
-def test_prefetch_gemm_bits(gemm, plan, qt, nested):
+def test_prefetch_gemm_bits(gemm, plan, qt, nested, side_form):
     rows, N, K = gemm
     assert _plan(rows, N, K)[:3] == plan
     dtype = torch.bfloat16
@@ -85,7 +99,7 @@ def test_prefetch_gemm_bits(gemm, plan, qt, nested):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", ["tail", "tiny", "ragged"])
-def test_prefetch_tail_and_edges(dtype, case):
+def test_prefetch_tail_and_edges(dtype, case, side_form):
     """tail: 2 k-tiles, so one side step in the loop and the rest after it; tiny: a 64 x 64 next weight (most
     workgroups own nothing); ragged: a next weight whose dwords do not fill the last workgroup's share."""
     rows, N, K = {"tail": (4096, 4096, 128), "tiny": (4096, 4096, 1024), "ragged": (2048, 4096, 4096)}[case]
@@ -179,3 +193,32 @@ def test_gemm_4bit_prefetch_same_weight_each_step_and_graph():
         gr.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, ref)
+
+
+def test_prefetch_tail_form_repeated_launches_and_streams():
+    """The tail form's work stealing: its per-stream chunk counter must be back at zero after every launch (the last
+    workgroup resets it), so back-to-back launches on one stream and launches on a second stream each dequantise every
+    chunk -- checked with a next weight of many chunks (11008 x 4096: 1,376 chunks on 256 workgroups, so most are
+    stolen) and a NaN-filled target each time; plus the 128 x 128 tile, which only the tail form runs."""
+    prev = lib.chgemm_set_side_mode(1)
+    try:
+        dtype = torch.bfloat16
+        g = torch.Generator(device="cuda").manual_seed(17)
+        q2, s2 = _weight(11008, 4096, dtype, "nf4", True, 19)
+        ref_w = F.dequantize_4bit(q2, s2)
+        for rows, N, K in ((4096, 4096, 1024), (512, 4096, 4096)):
+            X = torch.randn(rows, K, device="cuda", generator=g).to(dtype)
+            W = (torch.randn(N, K, device="cuda", generator=g) * 0.02).to(dtype)
+            ref_out = _plain_gemm(X, W)
+            for st in (torch.cuda.current_stream(), torch.cuda.Stream(), torch.cuda.current_stream()):
+                st.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(st):
+                    for _ in range(3):
+                        out, nxt = _pf_gemm(X, W, (q2, s2))
+                        st.synchronize()
+                        assert torch.equal(out, ref_out), (rows, N, K)
+                        assert torch.equal(nxt, ref_w.view_as(nxt)), (rows, N, K)
+                torch.cuda.current_stream().wait_stream(st)
+        assert _plan(512, 4096, 4096)[:2] == (4, 4)         # (the quarter tile took that one)
+    finally:
+        lib.chgemm_set_side_mode(prev)

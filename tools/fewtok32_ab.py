@@ -6,6 +6,8 @@ medians; plus a max-|diff| check of every arm against dequantize_4bit + matmul i
 Usage: python tools/fewtok32_ab.py [tokens ...]"""
 import os
 import sys
+os.environ.setdefault("BNB_HIP_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "bitsandbytes-sycl_amd", "build", "libbitsandbytes_hip_lab.so"))   # lab hooks: `make -C bitsandbytes-sycl_amd/csrc lab`
 
 import torch
 

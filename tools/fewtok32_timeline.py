@@ -4,6 +4,8 @@ relative to the earliest wave start: start, loads issued, table barrier, group 0
 Usage: python tools/fewtok32_timeline.py [M] [ABL extra bits, e.g. 7]"""
 import os
 import sys
+os.environ.setdefault("BNB_HIP_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "bitsandbytes-sycl_amd", "build", "libbitsandbytes_hip_lab.so"))   # lab hooks: `make -C bitsandbytes-sycl_amd/csrc lab`
 
 import numpy as np
 import torch

@@ -4,6 +4,8 @@ wide kernel with 1..4 chunks per lane), max |difference| to the first choice rel
 Usage: [GEMV_KNOBS=3,21,22,23,24] [GEMV_TWO_LDS=bytes] python tools/gemv_shape_probe.py [NxK ...]"""
 import os
 import sys
+os.environ.setdefault("BNB_HIP_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "bitsandbytes-sycl_amd", "build", "libbitsandbytes_hip_lab.so"))   # lab hooks: `make -C bitsandbytes-sycl_amd/csrc lab`
 
 import torch
 

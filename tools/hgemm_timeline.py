@@ -6,6 +6,8 @@ Usage: python tools/hgemm_timeline.py"""
 import ctypes as ct
 import os
 import sys
+os.environ.setdefault("BNB_HIP_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "bitsandbytes-sycl_amd", "build", "libbitsandbytes_hip_lab.so"))   # lab hooks: `make -C bitsandbytes-sycl_amd/csrc lab`
 
 import numpy as np
 

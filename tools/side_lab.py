@@ -4,6 +4,8 @@ kernel alone, their sum, and the prefetching GEMM under each chgemm_set_side_mod
 import ctypes as ct
 import os
 import sys
+os.environ.setdefault("BNB_HIP_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "bitsandbytes-sycl_amd", "build", "libbitsandbytes_hip_lab.so"))   # lab hooks: `make -C bitsandbytes-sycl_amd/csrc lab`
 import time
 
 import torch
