@@ -25,8 +25,6 @@
 #include "int8_common.hpp"
 
 #include <algorithm>
-#include <map>
-#include <mutex>
 #include <type_traits>
 #include <utility>
 
@@ -327,63 +325,64 @@ struct HgSide {
                              // the round-4 in-loop form instead of the tail form (below); lab ablations (timing only,
                              // wrong weights): 2 = no side stores, 8 = no consumption, 16 = no side loads, 32 = no side
                              // step in the loop, 64 = no tail
-  uint32_t* ticket;          // tail form: the launch's chunk counter + finished-workgroup counter (nullptr: static)
 };
 static int g_side_mode = 1;
 
 // Tail form of the side dequantise (round 6, V & HG_V_TAIL, the default of chgemm_tn_pf_*): no side work inside the
-// k-loop at all -- each workgroup, once its tile's epilogue has issued its C stores, dequantises chunks of the next
-// weight, taken first by its own index and then from a shared counter (work stealing) until none is left.  Why: the
-// k-loop ends up to ~8 % apart between the fastest and the slowest XCD on identical work (DESIGN.md §5 'Where k_hgemm's
-// fixed time goes': the same physical XCDs are slow in every shape and run), so with one tile per CU the fast XCDs idle
-// while the slow ones finish; here they spend that time on the next weight, and the next call runs its GEMM alone.
-// The in-loop form (round 4) paid for its side work in MFMA issue slots (+50 us at the metric shape); the tail form
-// takes no issue slot from any MFMA.  Values: exactly k_dequantize_4bit_stream's (code * absmax in fp32, one RNE cast;
-// nested: code2[q8] * absmax2 + offset) -- the same helper arithmetic as the in-loop form, whatever workgroup does a
-// chunk.  The counter pair is per stream (host: hg_tail_ticket) and reset by the last workgroup to finish, so the next
-// launch on that stream finds it at zero; under HIP-graph capture the launch takes the static assignment (chunk c to
-// workgroup c mod grid) instead, with no counter.
+// k-loop at all -- each wave, once its tile's epilogue has issued its C stores, dequantises its share of the next
+// weight.  The in-loop form (round 4) paid for its side work in MFMA issue slots (+40-50 us at the metric shape); the
+// tail form takes no issue slot from any MFMA, and the pipelined step costs what the unpipelined pair does
+// (profiles/lab/r06_tail_ab.txt: 258.9 vs 257.8 us; C4 18.08 vs 18.03 ms).  It was built to spend the XCD slack (the
+// k-loop ends up to ~8 % apart between the fastest and the slowest XCD on identical work) on the next
+// weight by work stealing; that lost (below).  Values: exactly k_dequantize_4bit_stream's (code * absmax in fp32, one RNE cast;
+// nested: code2[q8] * absmax2 + offset) -- the same helper arithmetic as the in-loop form, whatever wave does a chunk.
+// Chunk c (64 lanes x HG_TAIL_U packed dwords) goes to wave c mod waves (static; work stealing measured slower, below).
 constexpr int HG_V_TAIL = 524288;
-constexpr int HG_TAIL_U = 8;                               // 4-dword lane groups per wave chunk (256 dwords each)
+constexpr int HG_TAIL_U = 16;                              // packed dwords per lane per wave chunk
 
-// one wave's chunk c: HG_TAIL_U groups of 256 packed dwords (4 per lane, 32 weights, one statistics block); the loads
-// of a chunk land in w / am, hg_tail_store converts and stores them
+// one wave's chunk c: 64 x HG_TAIL_U packed dwords, lane l taking dwords 64 j + l (the k_dequantize_4bit_stream layout:
+// every load and every 16-B output store of the wave is one contiguous, whole-line run -- a lane-contiguous 16-B load
+// per lane made each store instruction write 16 B of every 64 and ran the tail ~3x slower)
 struct HgTailRegs {
-  hg_u32x4_t w[HG_TAIL_U];
-  float am[HG_TAIL_U];
+  uint32_t w[HG_TAIL_U];
+  uint32_t q[HG_TAIL_U];     // nested: the statistic's 8-bit code (decoded at store time, not at load time)
+  float a[HG_TAIL_U];        // nested: its second-level scale; plain: the fp32 absmax
 };
-__device__ __forceinline__ void hg_tail_load(const HgSide& side, const float* s_c2, float off, uint32_t c, int lane,
-                                             HgTailRegs& r) {
-  const uint32_t base = c * (256u * HG_TAIL_U);
+// issue the chunk's loads only -- nothing here consumes them, so the wave goes on to convert and store the previous
+// chunk while these are in flight (a statistic decoded here would make the wave wait for its load first)
+__device__ __forceinline__ void hg_tail_load(const HgSide& side, uint32_t c, int lane, HgTailRegs& r) {
+  const uint32_t base = c * (64u * HG_TAIL_U);
+  const uint32_t* Aw = reinterpret_cast<const uint32_t*>(side.packed);
 #pragma unroll
-  for (int u = 0; u < HG_TAIL_U; ++u) {
-    const uint32_t gd = min(base + 256u * u + 4u * (uint32_t)lane, (uint32_t)side.ndw - 4u);
-    r.w[u] = __builtin_nontemporal_load(reinterpret_cast<const hg_u32x4_t*>(side.packed + 4ull * gd));
-    const uint32_t blk = (gd * 8u) >> side.bs_shift;
-    r.am[u] = side.nested ? __fadd_rn(__fmul_rn(s_c2[side.q8[blk]], side.absmax2[blk >> side.bs2_shift]), off)
-                          : side.absmax[blk];
+  for (int j = 0; j < HG_TAIL_U; ++j) {
+    const uint32_t d = min(base + 64u * j + (uint32_t)lane, (uint32_t)side.ndw - 1u);
+    r.w[j] = __builtin_nontemporal_load(Aw + d);
+    const uint32_t blk = (d * 8u) >> side.bs_shift;
+    if (side.nested) {
+      r.q[j] = side.q8[blk];
+      r.a[j] = side.absmax2[blk >> side.bs2_shift];
+    } else {
+      r.a[j] = side.absmax[blk];
+    }
   }
 }
 template <typename T16>
-__device__ __forceinline__ void hg_tail_store(const HgSide& side, const float2* s_pair, uint32_t c, int lane,
-                                              const HgTailRegs& r) {
-  const uint32_t base = c * (256u * HG_TAIL_U);
+__device__ __forceinline__ void hg_tail_store(const HgSide& side, const float2* s_pair, const float* s_c2, float off,
+                                              uint32_t c, int lane, const HgTailRegs& r) {
+  const uint32_t base = c * (64u * HG_TAIL_U);
 #pragma unroll
-  for (int u = 0; u < HG_TAIL_U; ++u) {
-    const uint32_t gd = base + 256u * u + 4u * (uint32_t)lane;
-    if (gd >= (uint32_t)side.ndw) continue;               // (ndw % 4 == 0: a lane's 4 dwords are all in or all out)
+  for (int j = 0; j < HG_TAIL_U; ++j) {
+    const uint32_t d = base + 64u * j + (uint32_t)lane;
+    const float am = side.nested ? __fadd_rn(__fmul_rn(s_c2[r.q[j] & 0xFF], r.a[j]), off) : r.a[j];
+    hg_u32x4_t o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      hg_u32x4_t o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float2 p = s_pair[(r.w[u][j] >> (8 * i)) & 0xFF];
-        o[i] = cvt_pk<T16>(__fmul_rn(p.x, r.am[u]), __fmul_rn(p.y, r.am[u]));
-      }
-      // device-scope write-through (sc1), as k_dequantize_4bit_stream's default store policy: the next launch reads it
-      asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" : : "v"((gd + (uint32_t)j) * 16u), "v"(o),
-                   "s"(side.out) : "memory");
+    for (int i = 0; i < 4; ++i) {
+      const float2 p = s_pair[(r.w[j] >> (8 * i)) & 0xFF];
+      o[i] = cvt_pk<T16>(__fmul_rn(p.x, am), __fmul_rn(p.y, am));
     }
+    // device-scope write-through (sc1), as k_dequantize_4bit_stream's default store policy: the next launch reads it
+    if (d < (uint32_t)side.ndw)
+      asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" : : "v"(d * 16u), "v"(o), "s"(side.out) : "memory");
   }
 }
 
@@ -405,36 +404,26 @@ __device__ __forceinline__ void hg_side_tail(const HgSide& side, uint8_t* ep, in
     if (side.nested) s_c2[e] = side.code2[e];
   }
   const float off = side.nested ? *side.offset : 0.0f;
-  const uint32_t nchunks = (uint32_t)((side.ndw + 256 * HG_TAIL_U - 1) / (256 * HG_TAIL_U));
-  auto take = [&](uint32_t cur) -> uint32_t {             // the chunk after `cur` for this wave
-    if (side.ticket == nullptr) return cur + waves;
-    uint32_t t = 0;
-    if (lane == 0) t = waves + atomicAdd(side.ticket, 1u);
-    return __builtin_amdgcn_readfirstlane(t);
-  };
+  const uint32_t nchunks = (uint32_t)((side.ndw + 64 * HG_TAIL_U - 1) / (64 * HG_TAIL_U));
+  // static assignment: chunk c to wave c mod waves.  Work stealing was measured and dropped (profiles/lab/r06_tail_ab.txt):
+  // a wave that waits for a counter's return also waits for its previous chunk's stores (vmcnt counts both, in order),
+  // and that cost more than the XCD slack it recovered (one counter +40 us, eight per-XCD counters +12 us at the metric
+  // shape, against +1 us static)
+  // (the next chunk's loads are issued before this one is converted and stored: two register sets in rotation)
   HgTailRegs r0, r1;
   uint32_t c = wave_id;
   if (c < nchunks) {
-    hg_tail_load(side, s_c2, off, c, lane, r0);
+    hg_tail_load(side, c, lane, r0);
     while (true) {
-      const uint32_t n = take(c);
-      if (n < nchunks) hg_tail_load(side, s_c2, off, n, lane, r1);
-      hg_tail_store<T16>(side, s_pair, c, lane, r0);
+      const uint32_t n = c + waves;
+      if (n < nchunks) hg_tail_load(side, n, lane, r1);
+      hg_tail_store<T16>(side, s_pair, s_c2, off, c, lane, r0);
       if (n >= nchunks) break;
-      c = n;
-      const uint32_t n2 = take(c);
-      if (n2 < nchunks) hg_tail_load(side, s_c2, off, n2, lane, r0);
-      hg_tail_store<T16>(side, s_pair, c, lane, r1);
+      const uint32_t n2 = n + waves;
+      if (n2 < nchunks) hg_tail_load(side, n2, lane, r0);
+      hg_tail_store<T16>(side, s_pair, s_c2, off, n, lane, r1);
       if (n2 >= nchunks) break;
       c = n2;
-    }
-  }
-  if (side.ticket != nullptr && lane == 0) {
-    // the last wave to get here (every other one has taken its final chunk number) resets the pair for the next launch
-    // on this stream
-    if (atomicAdd(side.ticket + 1, 1u) == waves - 1) {
-      atomicExch(side.ticket, 0u);
-      atomicExch(side.ticket + 1, 0u);
     }
   }
 }
@@ -1258,37 +1247,6 @@ static void hgemm_launch_side(const HgPlan& pl, int m, int n, int k, const void*
   }
 }
 
-// The tail form's chunk counter pair for launches on the current stream of the current device (zeroed once; each launch's
-// last workgroup resets it).  Launches on one stream run one after another, so a pair is never shared by two launches
-// at once.  nullptr under HIP-graph capture (a captured launch would bake the pair in, and its replays could run beside
-// eager launches on the stream it was captured from) or when the allocation fails: the static chunk assignment then.
-static uint32_t* hg_tail_ticket() {
-  hipStream_t st = current_stream();
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, uint32_t*> pairs;
-  std::lock_guard<std::mutex> lock(mu);
-  const auto key = std::make_pair(dev, st);
-  const auto it = pairs.find(key);
-  if (it != pairs.end()) return it->second;
-  void* p = nullptr;
-  if (hipMalloc(&p, 2 * sizeof(uint32_t)) != hipSuccess || hipMemsetAsync(p, 0, 2 * sizeof(uint32_t), st) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  pairs[key] = static_cast<uint32_t*>(p);
-  return static_cast<uint32_t*>(p);
-}
-
 // false: a side dequantise was asked for that this kind / shape does not run (nothing launched)
 template <int OP, int V, int WI, int WJ>
 static bool hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void* A, long long lda, const void* B,
@@ -1300,7 +1258,6 @@ static bool hgemm_launch_shape(const HgPlan& pl, int m, int n, int k, const void
     if (side && !(g_side_mode & 128)) {
       HgSide sd = *side;
       sd.mode = g_side_mode;
-      sd.ticket = hg_tail_ticket();
       hgemm_launch_side<OP, V | HG_V_TAIL, WI, WJ, false>(pl, m, n, k, A, lda, B, ldb, C, ldc, rowStats, colStats, bias,
                                                           ws, sd);
       return true;

@@ -196,10 +196,9 @@ def test_gemm_4bit_prefetch_same_weight_each_step_and_graph():
 
 
 def test_prefetch_tail_form_repeated_launches_and_streams():
-    """The tail form's work stealing: its per-stream chunk counter must be back at zero after every launch (the last
-    workgroup resets it), so back-to-back launches on one stream and launches on a second stream each dequantise every
-    chunk -- checked with a next weight of many chunks (11008 x 4096: 1,376 chunks on 256 workgroups, so most are
-    stolen) and a NaN-filled target each time; plus the 128 x 128 tile, which only the tail form runs."""
+    """The tail form over a next weight of many chunks per wave (11008 x 4096: 2,752 chunks of 1,024 dwords on 1,024
+    waves), back to back on one stream and on a second stream, a NaN-filled target each time; plus the 128 x 128 tile
+    with split-K, which only the tail form runs."""
     prev = lib.chgemm_set_side_mode(1)
     try:
         dtype = torch.bfloat16
