@@ -10,6 +10,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -17,6 +18,10 @@ typedef uint16_t bf16_t;   // bfloat16 bit pattern
 typedef _Float16 fp16_t;   // IEEE binary16
 
 namespace bnb {
+
+// A process-global A/B or testing knob of the C-ABI setters (c*_set_*): an atomic, so a setter on one host thread and a
+// launch on another never race; a launch reads each knob once when it plans.  Knobs are per process, not per device.
+template <typename T> using Knob = std::atomic<T>;
 
 enum DataType { GENERAL8BIT = 0, FP4 = 1, NF4 = 2 };
 

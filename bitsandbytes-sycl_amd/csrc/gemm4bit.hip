@@ -157,7 +157,7 @@ k_gemm_4bit(int N, int M, int K, const T* __restrict__ A, const uint8_t* __restr
   }
 }
 
-int g_tile_override = 0;
+Knob<int> g_tile_override{0};
 
 // Split-K factor for the 256-tile kernel: enough workgroups to cover the 256 CUs when the output has
 // fewer than ~200 256x256 tiles (narrow column shards, e.g. N/8 = 512 features at M = 4096, or few

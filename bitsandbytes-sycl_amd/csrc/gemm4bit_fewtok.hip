@@ -458,8 +458,8 @@ k_gemm_4bit_fewtok(int N, int M, int K, const T* __restrict__ A, int lda, const 
 }
 
 // 0 = auto, 1 = off, 2 = forced wherever it fits (A/B knob; tests); >= 16: lab ablations
-int g_fewtok_mode = 0;
-extern int g_fewtoken_kernel;   // gemm4bit_wk.hip: != 0 selects one of the older few-token kernels
+Knob<int> g_fewtok_mode{0};
+extern Knob<int> g_fewtoken_kernel;   // gemm4bit_wk.hip: != 0 selects one of the older few-token kernels
 int skinny_cfg_knob();          // gemm4bit_skinny.hip: >= 0 forces a split-K geometry (lab A/B)
 
 bool fewtok_applicable(int m, int n, int k, int lda, int ldb, int blocksize, const void* A, const void* B) {

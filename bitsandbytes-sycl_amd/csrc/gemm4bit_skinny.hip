@@ -284,8 +284,8 @@ bool skinny_applicable(int m, int n, int k, int lda, int ldb, int blocksize, con
 // workgroups is mostly empty (11008 x 4096: 516 workgroups on 256 CUs, 30.2 -> 36.8 us at 48 rows); it is taken when
 // that round is at least 70 % full.  At 1..32 rows the 8-wave forms lost everywhere (same NB: +1..3 us; 2 x NB: +5..14 us).
 // g_skinny_cfg (cgemm_4bit_set_skinny_config, lab A/B): -1 = that rule, 0 = base, 1 = 8 waves same NB, 2 = 8 waves 2 x NB.
-static int g_skinny_cfg = -1;
-extern int g_fewtoken_kernel;   // gemm4bit_wk.hip
+static Knob<int> g_skinny_cfg{-1};
+extern Knob<int> g_fewtoken_kernel;   // gemm4bit_wk.hip
 int skinny_cfg_knob() { return g_skinny_cfg; }
 
 struct SkGeom {

@@ -770,22 +770,22 @@ constexpr int T64_MAX_TILES = 1024, T64_TICKET_SETS = 16;
 __device__ uint32_t g_t64_tickets[T64_TICKET_SETS * T64_MAX_TILES];
 
 // 0 = auto (33..64 tokens), 1 = off, 2 = forced wherever it applies (1..64 tokens; tests / A-B)
-int g_t64_mode = 0;
-int g_t64_ks = 0;                                            // lab: force the split count (0 = the rule)
+Knob<int> g_t64_mode{0};
+Knob<int> g_t64_ks{0};                                            // lab: force the split count (0 = the rule)
 // 1: in-kernel last-arriver combine, 0 (default): k_skinny_reduce.  Measured (tools/t64_time.py,
 // profiles/lab/r04_t64.txt): 11008 x 4096 at 64 rows 25.7 us in-kernel vs 22.6 us with the reduce launch -- the combine
 // of a row tile is one workgroup reading 192 KiB of device-scope partials (8.6 us of tail on 58 CUs), the reduce
 // launch spreads the same reads over ~700 workgroups for 5.7 us
-int g_t64_combine = 0;
+Knob<int> g_t64_combine{0};
 // partial-store policy (cgemm_4bit_set_t64_pstore): 2 = write-through 16-B lines by default -- the reduce launch's
 // boundary then has no dirty partials to write back (11008 x 4096 at 64 rows 22.9 -> 21.8 us, 4096 x 11008 24.7 ->
 // 22.3, 4096^2 19.0 -> 15.5; write-through dwords within 0.2 us of the lines; profiles/lab/r04_t64.txt)
-int g_t64_pstore = 2;
+Knob<int> g_t64_pstore{2};
 // waves per 48-row set (cgemm_4bit_set_t64_waves): 1 = the round-4 4-wave kernel, 2 = 8 waves, two per SIMD (round 5),
 // 0 = auto: 8 waves up to 48 tokens or where K is not split, 4 otherwise (round 5, 11008 x 4096 nested, graph replay over
 // 14 copies: 33 / 48 / 64 rows 20.13 / 21.37 / 21.77 us on 4 waves vs 18.92 / 20.47 / 22.28 on 8, profiles/lab/r05_ab.txt;
 // unsplit 28672 x 8192 at 64 rows 76.4 -> 72.0 us, profiles/lab/r05_t64r_ab.txt)
-int g_t64_kp = 0;
+Knob<int> g_t64_kp{0};
 
 // this launch's ticket set on the current device (nullptr: use the reduce launch).  Never during HIP-graph capture: a
 // captured launch would bake one ticket set into the graph, and its replays could then share counters with eager
@@ -817,7 +817,7 @@ static T64Geom t64_geometry(int m, int k) {
   int cus = device_cu_count();
   if (cus <= 0) cus = 256;
   int ks = std::max(1, std::min(ngr, cus / std::max(1, rt)));   // one round of workgroups on the CUs
-  if (g_t64_ks > 0) ks = std::min(ngr, g_t64_ks);
+  if (g_t64_ks > 0) ks = std::min(ngr, g_t64_ks.load());
   const int kc = (ngr + ks - 1) / ks;
   ks = (ngr + kc - 1) / kc;
   return {rt, ks, kc};
@@ -838,7 +838,7 @@ bool t64_applicable(int m, int n, int k, int lda, int ldb, int blocksize, int bl
 // reduce on every shape, growing with the token rows -- every workgroup pulls all 64 x K token values through its
 // vector-memory path, 4x the LDS-DMA form's 64 x K/4 (profiles/lab/r05_t64r_ab.txt; a rotated group order per workgroup,
 // against L2-channel camping of the 16 same-channel token rows of one load, changed nothing)
-int g_t64r = 1;
+Knob<int> g_t64r{1};
 static bool t64r_route(int m, int k, const SkStats& st, bool nested) {
   if (g_t64r == 1 || g_t64_mode >= 15) return false;         // (the LDS-DMA form's labs keep their kernel)
   if (nested ? ((uintptr_t)st.q8 & 3) != 0 : ((uintptr_t)st.absmax & 15) != 0) return false;
@@ -881,7 +881,7 @@ bool launch_gemm_4bit_t64(int m, int n, int k, const T* A, int lda, const uint8_
   st.bs2_shift = nested ? __builtin_ctz(blocksize2) : 0;
   const dim3 grid((unsigned)(geo.row_tiles * geo.ksplit));
   uint32_t* tickets = geo.ksplit > 1 && g_t64_mode != 15 ? t64_tickets(geo.row_tiles, (long long)geo.ksplit * n * m * 4) : nullptr;
-  const int pstore = (long long)geo.ksplit * n * m * 4 <= 0x7FFFFFFFLL ? g_t64_pstore : 0;
+  const int pstore = (long long)geo.ksplit * n * m * 4 <= 0x7FFFFFFFLL ? g_t64_pstore.load() : 0;
   auto lab = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(T64_THREADS), 0, current_stream(), m, n, k, A, lda, B, ldb, st, code, out, ldc, ws,
                        geo.ksplit, geo.kc, tickets, pstore);

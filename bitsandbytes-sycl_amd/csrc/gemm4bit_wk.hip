@@ -155,7 +155,7 @@ k_gemm_4bit_wk(int N, int M, int K, const T* __restrict__ A, int lda, const uint
 int device_cu_count();      // CUs of the current device (cached; gemv4bit.hip)
 // 0 = auto (this kernel at <= WK_MAX_TOKENS tokens on narrow weights, else the split-K kernel), 1 = the split-K
 // skinny kernel only, 2 = this kernel for every shape it fits (A/B knob; tests)
-int g_fewtoken_kernel = 0;
+Knob<int> g_fewtoken_kernel{0};
 constexpr int WK_MAX_TOKENS = 6;
 
 bool wk_applicable(int m, int n, int k, int lda, int ldb, int blocksize, const void* A, const void* B) {

@@ -74,7 +74,7 @@ __device__ __forceinline__ int xcd_remap(int wg, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (wg >> 3);
 }
 
-extern int g_tile_override;   // 0 = auto, 128 / 256 = force that tile kernel (tests / A-B benchmarks)
+extern Knob<int> g_tile_override;   // 0 = auto, 128 / 256 = force that tile kernel (tests / A-B benchmarks)
 
 // ws/ksplit: split-K over ksplit workgroups per tile with fp32 partials in ws[ksplit][n][m]
 // (ksplit == 1: ws unused, direct T output)

@@ -37,8 +37,8 @@ struct PlanKey {
 std::mutex g_mu;
 std::map<PlanKey, int> g_plans;                 // solution index (rocBLAS lists negative ones too); 0 = standard
 std::map<int, rocblas_handle> g_handles;        // per device
-int g_search = 1;                               // 0: never search (standard algorithm only)
-double g_budget_ms = 2000.0;                    // search time per shape (230 solutions at 4096 x 11008 x 4096: ~1 s)
+Knob<int> g_search{1};                               // 0: never search (standard algorithm only)
+Knob<double> g_budget_ms{2000.0};                    // search time per shape (230 solutions at 4096 x 11008 x 4096: ~1 s)
 constexpr double kSearchMinFlop = 1e10;         // smaller problems keep the standard algorithm (nothing to win)
 
 int rows_bucket(int m) {

@@ -267,12 +267,12 @@ constexpr int GB_TABLE_BYTES = 65536;
 // nested statistics decoded where each chunk is consumed (LAZY, round 5) or all up front (the round-4 form, default; A/B
 // knob cgemv_4bit_set_lazy_nested).  Measured and rejected: bit-identical, +0.2..+1.9 % (11008 x 4096 8.25 -> 8.34 us;
 // tools/r05_gemv_lazy_ab.py, profiles/lab/r05_gemv_lazy_ab.txt)
-static int g_gv_lazy = 0;
+static Knob<int> g_gv_lazy{0};
 constexpr int GB_MAX_WAVES = 16;
 // two workgroups per CU up to 79 KiB (K <= 7680), and at exactly half the CU's 160 KiB (K = 8192) from 2048 rows:
 // 3584 / 4096 / 8192 x 8192 6.20 / 6.79 / 10.77 -> 6.00 / 6.34 / 10.43 us, but 1024 x 8192 4.00 -> 5.04 us, where
 // two table fills per CU outweigh the gain (profiles/lab/r02_gemv_wide.txt).  Lab knob: cgemv_4bit_set_two_per_cu_lds.
-static size_t g_gb_two_per_cu_lds = 79 * 1024;
+static Knob<size_t> g_gb_two_per_cu_lds{79 * 1024};
 constexpr size_t GB_HALF_CU_LDS = 80 * 1024;
 constexpr int GB_HALF_CU_MIN_ROWS = 2048;
 
@@ -565,8 +565,8 @@ k_gemv_4bit_generic(int M, int K, const T* __restrict__ A, const uint8_t* __rest
 // 0 = auto (k_gemv_4bit_wide on narrow / long-K weights, k_gemv_4bit_bal where it fits, else k_gemv_4bit_dot),
 // 1 = k_gemv_4bit_dot only, 2 = k_gemv_4bit_wide wherever it applies, 3 = auto without the wide kernel (A/B, tests);
 // 20 + U: the wide kernel with U chunks per lane (lab)
-int g_gemv_kernel = 0;
-int g_gemv_wide_rows = 0;   // 1: the wide kernel one row per workgroup (A/B, tests)
+Knob<int> g_gemv_kernel{0};
+Knob<int> g_gemv_wide_rows{0};   // 1: the wide kernel one row per workgroup (A/B, tests)
 
 int device_cu_count() {
   static int cus = 0;

@@ -177,12 +177,12 @@ constexpr int HG_V = 16 + 8192;
 // 126.3 -> 124.8 us, config 3 52.7 -> 51.7 us, the NF4 step unchanged to -1 us, C4 unchanged;
 // profiles/lab/r04_store_policy.txt)
 constexpr int HG_V_CWT = 32768;
-static int g_hg_cwt = 1;
+static Knob<int> g_hg_cwt{1};
 // variant bit: the 16-bit full-tile epilogue interleaved per 16-row group -- group i's outputs are converted (the bf16 /
 // fp16 casts, or int8's mm_dequant) and staged while group i - 1's rows are read back and stored, so the VALU of the
 // conversion overlaps the store stream instead of preceding all of it (chgemm_set_epilogue; round 5)
 constexpr int HG_V_EPI = 65536;
-static int g_hg_epi = 1;
+static Knob<int> g_hg_epi{1};
 // variant bit (with HG_V_EPI only): the interleaved epilogue's C stores carry the non-temporal hint (nt), so the output
 // (not re-read by this step) does not displace the operands in the last-level cache (chgemm_set_c_store(2); A/B arm)
 constexpr int HG_V_CNT = 131072;
@@ -326,7 +326,7 @@ struct HgSide {
                              // wrong weights): 2 = no side stores, 8 = no consumption, 16 = no side loads, 32 = no side
                              // step in the loop, 64 = no tail
 };
-static int g_side_mode = 1;
+static Knob<int> g_side_mode{1};
 
 // Tail form of the side dequantise (round 6, V & HG_V_TAIL, the default of chgemm_tn_pf_*): no side work inside the
 // k-loop at all -- each wave, once its tile's epilogue has issued its C stores, dequantises its share of the next
@@ -1181,8 +1181,8 @@ constexpr double HG_HALF_KT = 0.6;
 // the 128 x 128 tile (round 5, 16-bit kinds, no side dequantise): a quarter of the 256 x 256 tile's MFMAs per k-tile with
 // twice its copies and fragment reads per MFMA; its k-tile time in 256 x 256 k-tile units (lab-calibrated,
 // chgemm_set_quarter_tile)
-static double g_hg_quarter_kt = 0.40;
-static int g_hg_quarter = 1;             // 0 = never, 1 = by cost (default), 2 = forced where allowed (tests / A-B)
+static Knob<double> g_hg_quarter_kt{0.40};
+static Knob<int> g_hg_quarter{1};             // 0 = never, 1 = by cost (default), 2 = forced where allowed (tests / A-B)
 struct HgPlan {
   int wi, wj, splits, kchunk;
 };
@@ -1200,7 +1200,7 @@ static HgPlan hgemm_plan(int m, int n, int k, int elem, bool allow_split, bool f
   double best_cost = 1e300;
   for (int si = forced ? 3 : 0; si < (full_tiles_only ? 1 : quarter ? 4 : 3); ++si) {
     const int wi = shapes[si][0], wj = shapes[si][1];
-    const double tkt = (wi == 8 && wj == 8) ? 1.0 : (wi == 4 && wj == 4) ? g_hg_quarter_kt : HG_HALF_KT;
+    const double tkt = (wi == 8 && wj == 8) ? 1.0 : (wi == 4 && wj == 4) ? g_hg_quarter_kt.load() : HG_HALF_KT;
     const long long tiles = (long long)((m + 32 * wi - 1) / (32 * wi)) * ((n + 32 * wj - 1) / (32 * wj));
     double cost = (double)((tiles + cus - 1) / cus) * nkt * tkt;
     if (cost < best_cost) {

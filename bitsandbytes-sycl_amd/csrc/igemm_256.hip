@@ -285,7 +285,7 @@ k_igemm_splitk_reduce(const int32_t* __restrict__ ws, int ksplit, int M, int N, 
   }
 }
 
-static int g_igemm_splitk = -1;   // < 0: auto; 1 = never split; >= 2: force that factor where it applies (tests)
+static Knob<int> g_igemm_splitk{-1};   // < 0: auto; 1 = never split; >= 2: force that factor where it applies (tests)
 
 // Split-K factor for a row-major 256-tile problem: enough workgroups for the 256 CUs when the output has fewer
 // than ~200 tiles, with at least 8 k-tiles (1024 k) per split -- 2 below 256 rows (few-token forwards, where the

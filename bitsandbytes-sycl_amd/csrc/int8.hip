@@ -294,7 +294,7 @@ constexpr int RQ_MAX_VEC = 32;   // 16-B vectors per lane: K <= 16384
 typedef uint32_t rq_u32x2_t __attribute__((ext_vector_type(2)));
 // cint8_set_row_quant_store; off: measured neutral (row quantise 30.5 vs 30.7 us, + igemmlt 156.7 vs 156.8 us at
 // 4096 x 11008; the 90 MB fp16 read, not the 45 MB int8 write, sets its time; profiles/lab/r04_store_policy.txt)
-static int g_rq_wt = 0;
+static Knob<int> g_rq_wt{0};
 
 // NV = 16-B vectors per lane (the smallest instance that holds the row: registers decide how many rows a CU keeps in
 // flight -- 32 vectors cost 171 VGPRs, two waves per SIMD)
@@ -619,7 +619,7 @@ k_igemm(int M, int N, int K, const int8_t* __restrict__ A, const int8_t* __restr
   }
 }
 
-static int g_igemm_tile = 0;   // 0 = auto, 128 = force the 128x128 register-staged kernel, 4 = force the 4-wave
+static Knob<int> g_igemm_tile{0};   // 0 = auto, 128 = force the 128x128 register-staged kernel, 4 = force the 4-wave
                                // hgemm.hip kernel for row-major operands, 8 = force the 8-wave igemm_256 (tests / A-B)
 
 template <int AF, int BF, int EPI>

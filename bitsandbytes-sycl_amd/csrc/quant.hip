@@ -437,12 +437,12 @@ void quantize_blockwise(const float* code, const T* A, float* absmax, uint8_t* o
 // then leaves no dirty L2 lines for the kernel end / boundary to write back: the dequantise alone 23.1 -> 14.9 us, the
 // metric step 263.3 -> 260.2 us, C1 8.85 -> 8.6 us; non-temporal stores 20.8 us alone but a slower step (266.0)
 // (tools/dequant_store_ab.py, tools/bench_knobs.py; profiles/lab/r04_store_policy.txt)
-static int g_dq_p = 8, g_dq_grid_cap = 0, g_dq_store = 2;
+static Knob<int> g_dq_p{8}, g_dq_grid_cap{0}, g_dq_store{2};
 // scalar-loaded nested statistics (SQ above; cdequantize_set_nested_scalar): 1 = where they apply, 0 = off (default).
 // Measured and rejected (round 5, tools/r05_epi_ab.py, profiles/lab/r05_ab.txt): bit-identical, but the metric weight's
 // dequantise takes 30.6 us against 15.1 us with the per-lane loads (back to back), the metric step 265.5 vs 258.0 us --
 // each wave waits on its scalar loads before any of its math, where the per-lane loads overlap across waves.
-static int g_dq_sq = 0;
+static Knob<int> g_dq_sq{0};
 template <typename T, int DT, bool NESTED>
 static void launch_dq_stream(const uint8_t* A, const float* absmax, T* out, int bs_shift, long long ndw,
                              const NestedStats& ns) {
