@@ -1,4 +1,7 @@
-"""A/B of the k_hgemm schedules (chgemm_set_variant 0 = default, 1 = the alternative arm) on the library's own entry
+"""(Historical, round 6: chgemm_set_variant and the round-3 schedule arm it selected were removed from the library --
+see DESIGN.md §2; this lab is kept as the record of the measurements it produced.)
+
+A/B of the k_hgemm schedules (chgemm_set_variant 0 = default, 1 = the alternative arm) on the library's own entry
 points, interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24): bf16 chgemm_tn at the metric shape
 and the int8 igemmlt + dequant on the 4-wave body (cigemm_set_tile(4)) against the 8-wave igemm_256 (tile 8).  Outputs
 of every arm are compared bit for bit.  Usage: python tools/hgemm_variant_ab.py [rounds]"""

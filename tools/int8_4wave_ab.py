@@ -1,4 +1,7 @@
-"""A/B: the int8 igemmlt+dequant on the 4-wave kernel (hgemm.hip HG_I8_DEQ, forced by cigemm_set_tile(4)) against
+"""(Historical, round 6: chgemm_set_variant and the round-3 schedule arm it selected were removed from the library --
+see DESIGN.md §2; this lab is kept as the record of the measurements it produced.)
+
+A/B: the int8 igemmlt+dequant on the 4-wave kernel (hgemm.hip HG_I8_DEQ, forced by cigemm_set_tile(4)) against
 the 8-wave igemm_256 (the default, cigemm_set_tile(0)), interleaved rounds in one process; bit-identity of the two outputs (both
 are exact int32 + the same mm_dequant) and of the int32 products.  Usage: python tools/int8_4wave_ab.py [rounds]"""
 import os

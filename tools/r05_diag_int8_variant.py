@@ -1,4 +1,7 @@
-"""Diagnostic: int8 igemmlt + dequant on the 4-wave k_hgemm, default schedule vs the round-3 arm (chgemm_set_variant(1)),
+"""(Historical, round 6: chgemm_set_variant and the round-3 schedule arm it selected were removed from the library --
+see DESIGN.md §2; this lab is kept as the record of the measurements it produced.)
+
+Diagnostic: int8 igemmlt + dequant on the 4-wave k_hgemm, default schedule vs the round-3 arm (chgemm_set_variant(1)),
 interleaved epilogue on / off, and the 8-wave igemm_256, at 4096 x 4096 x 11008: which pairs are bit-identical, how
 many elements differ, and whether each arm is deterministic over repeats."""
 import os
