@@ -118,21 +118,33 @@ PREFETCH = [False]
 
 
 class StepClock:
-    """Step boundaries of the timed region as one chain of HIP events on the launching stream: one record
-    before the first step and one after each (K + 1 in all), so step i lasts ev[i] -> ev[i+1] and the
-    median over the K steps comes without a second event per step."""
+    """Step boundaries of the timed region as HIP events on the launching stream, recorded only around the sampled
+    steps (every `every`-th), so a sampled step i lasts ev[i] -> ev[i+1].
+    An event record between two kernels costs the stream ~3-4 us (tools/step_overhead.py), so a record at every one of
+    the K + 1 boundaries cost ~1 % of the metric step; the sampled form keeps the median without it (round 6)."""
 
-    def __init__(self, steps):
-        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    def __init__(self, steps, every=1):
+        self.every = max(1, every) if steps >= 2 * every else 1     # (short runs: every step)
+        # sampled steps: i % every == every // 2, i.e. not the steps that carry the stage events (i % every == 0);
+        # the events are made (and first recorded: the HIP event is created then) up front, not inside the timed steps
+        self.off = self.every // 2
+        self.ev = {b: torch.cuda.Event(enable_timing=True) for b in range(steps + 1)
+                   if self.every == 1 or (b - self.off) % self.every in (0, 1)}
+        for e in self.ev.values():
+            e.record()
+        torch.cuda.synchronize()
         self.n = 0
 
     def mark(self):
-        self.ev[self.n].record()
+        e = self.ev.get(self.n)
+        if e is not None:
+            e.record()
         self.n += 1
 
     def median_ms(self):
         import statistics
-        return statistics.median(a.elapsed_time(b) for a, b in zip(self.ev[:self.n - 1], self.ev[1:self.n]))
+        return statistics.median(self.ev[b].elapsed_time(self.ev[b + 1]) for b in sorted(self.ev)
+                                 if (b - self.off) % self.every == 0 and b + 1 in self.ev and b + 1 < self.n)
 
 
 def _time_loop(fn, iters, warmup=3, prewarm_s=0.0):
@@ -439,13 +451,15 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
     # rank 0 keeps the full CB / SCB for the world-1 sample check after the timed region (verify_sharded_output)
     check = int8_world1_sample(A, CB, SCB, sample_rows(m)) if world > 1 and rank == 0 else None
     del CB
-    clock = StepClock(steps)
+    # (no per-step event chain here: an event record between two kernels costs the stream ~3-4 us, 2-3 % of this step;
+    # the world-1 step writes into a preallocated output like a model's static buffer)
+    out_local = torch.empty(m, lin.end - lin.start, dtype=torch.float16, device=dev) if world == 1 else None
 
     def step():
         if world > 1:
             lin.forward(A, assemble=True, chunks=chunks)
         else:
-            lin.forward_local(A)
+            lin.forward_local(A, out=out_local)
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -453,10 +467,8 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    clock.mark()
     for _ in range(steps):
         step()
-        clock.mark()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -468,9 +480,7 @@ def bench_int8_sharded(dev, world, rank, steps, warmup, chunks, m=M, n=N, k=K):
         elapsed = t.item()
     per = elapsed / steps
     ops = 2.0 * m * n * k
-    med = clock.median_ms() * 1e-3
     res = {"shape": [m, n, k], "n_gpus": world, "tops": ops / per / 1e12, "ms_per_step": per * 1e3,
-           "median_step_ms_rank0": med * 1e3,
            "step": "int8_row_quant(X) + fused igemmlt+dequant on this rank's CB rows" +
                    (f" + {backend_label()} all_gather ({chunks} chunks) + [M, N] assembly" if world > 1 else ""),
            "frac_of_int8_peak": ops / per / 1e12 / PEAK_INT8_TOPS}
@@ -1151,7 +1161,7 @@ def main():
 
     library = dequant_route(gemm_kernel_name(Mc, shard))
 
-    clock = StepClock(args.steps)
+    clock = StepClock(args.steps, STAGE_EVERY)
     F.reserve_stage_events(3 * (args.steps // STAGE_EVERY + 1))   # the sampled steps' stage events, made up front
 
     def step(record=False):
