@@ -276,11 +276,33 @@ static Knob<size_t> g_gb_two_per_cu_lds{79 * 1024};
 constexpr size_t GB_HALF_CU_LDS = 80 * 1024;
 constexpr int GB_HALF_CU_MIN_ROWS = 2048;
 
+#ifdef BNB_LAB
+// lab build only (make lab): per-wave s_memrealtime stamps (10 ns ticks) of k_gemv_4bit_bal at
+// g_gv_tl[(blockIdx.x * GB_MAX_WAVES + wave) * 8 + i]: 0 start, 1 statistics / activation loads issued (first barrier),
+// 2 weight loads issued, 3 statistics + activations landed and the table built (second barrier), 4 last chunk's dots
+// done, 5 row stored, 6 the wave's XCD (HW_REG_XCC_ID), 7 block id (cgemv_4bit_timeline; tools/r06_gemv_timeline.py)
+__device__ unsigned long long* g_gv_tl = nullptr;
+__device__ int g_gv_abl = 0;   // lab A/B bits (cgemv_4bit_lab_bits): 1 = no barrier between the statistics / activation
+                               // issue and the weight issue
+__device__ __forceinline__ unsigned long long gv_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define GV_TL(i) tl[i] = gv_now()
+#else
+#define GV_TL(i) ((void)0)
+#endif
+
 template <typename T, int R, int U, bool NESTED, bool LAZY = true>
 __global__ void __launch_bounds__(GB_MAX_WAVES * 64)
 k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
                 const float* __restrict__ datatype, T* __restrict__ out, int ldb, int G) {
   extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
+#ifdef BNB_LAB
+  unsigned long long tl[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  GV_TL(0);
   uint8_t* table = gsm;                               // GB_TABLE_BYTES
   uint8_t* xs = gsm + GB_TABLE_BYTES;                 // K * 2 bytes, swizzled
   // nested code map entry t in the unused upper half of table row t >> 5 (the copies fill bytes 0..127 of each
@@ -327,7 +349,11 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
     const int i = p * 64 + lane, c = i >> 2;
     if (i < nx) glds16(A + 8 * (4 * c + (((i & 3) - (c >> 2)) & 3)), xs + p * 1024);
   }
+#ifdef BNB_LAB
+  if (!(g_gv_abl & 1))
+#endif
   __builtin_amdgcn_s_barrier();                       // all statistics / activation requests are out
+  GV_TL(1);
   // (2) this wave's weights, non-temporal, consumption order
   uintptr_t bp = (uintptr_t)B;
   asm volatile("" : "+s"(bp)::"memory");
@@ -340,6 +366,7 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
           __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row_of(j) * ldb + 16LL * chunk_of(u)));
       b[u][j] = make_uint4(v.x, v.y, v.z, v.w);
     }
+  GV_TL(2);
   // (3) table: thread t < 256 writes entry t (32 copies, 16-B stores rotated by t to spread the banks)
   for (int t = threadIdx.x; t < 256; t += NW * 64) {
     float hi = dt[0], lo = dt[0];
@@ -359,6 +386,7 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * U) : "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
+  GV_TL(3);
   // (nested, LAZY: each block's absmax is decoded where its chunk is consumed, so the code-map reads and the decode of
   // later chunks overlap the lookups of earlier ones instead of all preceding the first dot)
   if constexpr (NESTED && !LAZY) {
@@ -400,6 +428,7 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
       acc[j] += valid ? part : 0.0f;
     }
   }
+  GV_TL(4);
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[j] = wave_sum(acc[j]);
   if (lane == 0) {
@@ -409,6 +438,18 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
       if (row < r1) out[row] = Io<T>::from_f32(acc[j]);
     }
   }
+#ifdef BNB_LAB
+  if (g_gv_tl != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GV_TL(5);
+    if (lane == 0) {
+      unsigned long long* o = g_gv_tl + ((long long)blockIdx.x * GB_MAX_WAVES + wave) * 8;
+      for (int i = 0; i < 6; ++i) o[i] = tl[i];
+      o[6] = (unsigned long long)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15);
+      o[7] = blockIdx.x;
+    }
+  }
+#endif
 }
 
 // Wide GEMV (narrow or long-K weights: the 70B shards, e.g. 1024 x 28672 and 128 x 8192): one workgroup per weight
@@ -773,6 +814,12 @@ void cgemv_4bit_set_kernel(int which) { bnb::g_gemv_kernel = which; }
 void cgemv_4bit_set_wide_rows(int mode) { bnb::g_gemv_wide_rows = mode; }
 // [lab, not in the header] LDS bytes up to which the balanced GEMV runs two workgroups per CU (default 80 KiB)
 #ifdef BNB_LAB
+int cgemv_4bit_timeline(unsigned long long* buf) {   // [lab build only] k_gemv_4bit_bal stamps (nullptr: off)
+  return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_gv_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+int cgemv_4bit_lab_bits(int v) {                      // [lab build only] g_gv_abl
+  return hipMemcpyToSymbol(HIP_SYMBOL(bnb::g_gv_abl), &v, sizeof(v)) == hipSuccess ? 0 : 1;
+}
 void cgemv_4bit_set_two_per_cu_lds(int bytes) { bnb::g_gb_two_per_cu_lds = (size_t)bytes; }   // [lab build only]
 #endif
 // [additive, testing] nested statistics of the balanced GEMV decoded where each chunk is consumed (1) or all before the
