@@ -252,7 +252,7 @@ k_gemv_4bit_dot(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
 // r02_gemv_floor.txt): k_gemv_4bit_dot spends ~1/4 of its time before its first dot (its workgroups wait for
 // activations and statistics queued behind other workgroups' weight requests) and is then bound by the
 // table lookups' LDS and VALU issue.  This kernel changes four things, arithmetic unchanged (bit-identical):
-//   * G = 2 x CUs workgroups, workgroup g owns rows [g*M/G, (g+1)*M/G) (22 at 11008): every CU gets the same
+//   * G = 2 x CUs workgroups, workgroup g owns M / G rows, one more for g < M % G (21-22 at 11008): every CU gets the same
 //     work, NW = ceil(rows / R) waves take rows r0 + w + NW*j (j < R);
 //   * the table lookup address is ONE v_perm_b32 of {packed dword, lane byte}: entry e of copy c at byte
 //     256 e + 4 c (32 copies over a 64 KiB span; lanes l and l+32 share copy l & 31, different 32-lane groups),
@@ -296,8 +296,8 @@ __device__ __forceinline__ unsigned long long gv_now() {
 
 template <typename T, int R, int U, bool NESTED, bool LAZY = true>
 __global__ void __launch_bounds__(GB_MAX_WAVES * 64)
-k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict__ B, GemvStats st,
-                const float* __restrict__ datatype, T* __restrict__ out, int ldb, int G) {
+k_gemv_4bit_bal(const uint8_t* __restrict__ B, const T* __restrict__ A, const float* __restrict__ datatype,
+                T* __restrict__ out, int q, int rem, int ldb, int K, int NW, GemvStats st) {
   extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
 #ifdef BNB_LAB
   unsigned long long tl[6] = {0, 0, 0, 0, 0, 0};
@@ -312,12 +312,38 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
   };
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int NW = blockDim.x >> 6;
-  const int r0 = (int)((long long)blockIdx.x * M / G), r1 = (int)((long long)(blockIdx.x + 1) * M / G);
+  // rows [r0, r1): q + 1 rows for the first `rem` workgroups, q for the rest (no division in the kernel)
+  const int bid = blockIdx.x;
+  const int r0 = bid * q + min(bid, rem), r1 = r0 + q + (bid < rem ? 1 : 0);
   const int nch = K >> 5;
   const long long two_ldb = 2LL * ldb;
   auto row_of = [&](int j) { return min(r0 + wave + NW * j, r1 - 1); };
   auto chunk_of = [&](int u) { return min(lane + 64 * u, nch - 1); };
+  // this wave's weights, non-temporal, consumption order
+  uint4 b[U][R];
+  auto issue_weights = [&]() {
+    uintptr_t bp = (uintptr_t)B;
+    asm volatile("" : "+s"(bp)::"memory");
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const u32x4_t v =
+            __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row_of(j) * ldb + 16LL * chunk_of(u)));
+        b[u][j] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+  };
+#if defined(BNB_LAB)
+  const bool wfirst = (g_gv_abl & 2) != 0;            // lab A/B: the weights before the statistics and activations
+#elif defined(BNB_GV_WFIRST)
+  constexpr bool wfirst = BNB_GV_WFIRST != 0;
+#else
+  constexpr bool wfirst = false;
+#endif
+  if (wfirst) {
+    issue_weights();
+    asm volatile("" ::: "memory");
+  }
 
   // (1) code values (scalar), block statistics, activations by LDS-DMA (lane i of the instruction for LDS
   //     slot i = 16 B fetches the piece that belongs there under the swizzle)
@@ -349,23 +375,16 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
     const int i = p * 64 + lane, c = i >> 2;
     if (i < nx) glds16(A + 8 * (4 * c + (((i & 3) - (c >> 2)) & 3)), xs + p * 1024);
   }
+  if (wfirst) {
+    GV_TL(1);
+  } else {
 #ifdef BNB_LAB
-  if (!(g_gv_abl & 1))
+    if (!(g_gv_abl & 1))
 #endif
-  __builtin_amdgcn_s_barrier();                       // all statistics / activation requests are out
-  GV_TL(1);
-  // (2) this wave's weights, non-temporal, consumption order
-  uintptr_t bp = (uintptr_t)B;
-  asm volatile("" : "+s"(bp)::"memory");
-  uint4 b[U][R];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const u32x4_t v =
-          __builtin_nontemporal_load((gvec_p)((gbyte_p)bp + (long long)row_of(j) * ldb + 16LL * chunk_of(u)));
-      b[u][j] = make_uint4(v.x, v.y, v.z, v.w);
-    }
+    __builtin_amdgcn_s_barrier();                     // all statistics / activation requests are out
+    GV_TL(1);
+    issue_weights();                                  // (2)
+  }
   GV_TL(2);
   // (3) table: thread t < 256 writes entry t (32 copies, 16-B stores rotated by t to spread the banks)
   for (int t = threadIdx.x; t < 256; t += NW * 64) {
@@ -383,7 +402,8 @@ k_gemv_4bit_bal(int M, int K, const T* __restrict__ A, const uint8_t* __restrict
     if (threadIdx.x < 256) code2s_at(threadIdx.x) = c2;
     for (int t = threadIdx.x + NW * 64; t < 256; t += NW * 64) code2s_at(t) = st.code2[t];   // < 4 waves
   }
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * U) : "memory");
+  if (wfirst) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * U) : "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
   GV_TL(3);
@@ -646,7 +666,8 @@ static bool launch_gemv_bal(int m, int k, const T* A, const uint8_t* B, const Ge
   if (!two && R > 1) return false;
   const int nw = (rows + R - 1) / R;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(G), dim3(64 * nw), lds, current_stream(), m, k, A, B, st, datatype, out, ldb, G);
+    hipLaunchKernelGGL(kern, dim3(G), dim3(64 * nw), lds, current_stream(), B, A, datatype, out, m / G, m % G, ldb, k,
+                       nw, st);
     return true;
   };
   auto pick = [&](auto lz) {

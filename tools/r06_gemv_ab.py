@@ -25,7 +25,7 @@ def main():
             W = (torch.randn(n_out, k_in, device=dev, generator=g) * 0.02).to(torch.bfloat16)
             ws.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True))
             del W
-        arms = {"default": 0, "no_issue_barrier": 1}
+        arms = {"default": 0, "no_issue_barrier": 1, "weights_first": 2}
         times = {a: [] for a in arms}
         refs = {}
         for rnd in range(6):

@@ -1,5 +1,5 @@
 """Per-wave timeline of the decode GEMV k_gemv_4bit_bal, lab build only:
-BNB_HIP_LIBRARY=<lab .so> python tools/r06_gemv_timeline.py
+BNB_HIP_LIBRARY=<lab .so> [GV_LAB_BITS=<cgemv_4bit_lab_bits>] python tools/r06_gemv_timeline.py
 
 Config 2 (Linear4bit NF4 11008 x 4096, nested statistics, bf16), 14 rotating weight copies launched back to back (the
 bench leg's setting: > the 256 MB MALL, so the weights come from HBM); the stamps of the LAST launch are read (every
@@ -33,6 +33,7 @@ def main():
         ws.append(F.quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True))
         del W
     buf = torch.zeros(4096 * 16 * 8, dtype=torch.int64, device=dev)
+    assert F.lib.cgemv_4bit_lab_bits(ct.c_int(int(os.environ.get("GV_LAB_BITS", "0")))) == 0
     for q, st in ws:                                        # warm: code objects, plans
         F.gemv_4bit(x, q.t(), out=out, state=st)
     torch.cuda.synchronize()
