@@ -16,7 +16,9 @@ import python_src_quants.functional as F  # noqa: E402
 def main():
     dev = torch.device("cuda", 0)
     res = {"lib": os.path.basename(os.environ.get("BNB_HIP_LIBRARY", "product"))}
-    for n_out, k_in, nested in ((11008, 4096, True), (11008, 4096, False), (4096, 4096, True), (4096, 11008, True)):
+    shapes = ((11008, 4096, True), (11008, 4096, False), (4096, 4096, True), (4096, 11008, True),
+              (1280, 8192, True), (7168, 8192, True), (1024, 28672, True), (128, 8192, True))   # + the 70B rank shards
+    for n_out, k_in, nested in shapes:
         g = torch.Generator(device=dev).manual_seed(2)
         x = torch.randn(1, k_in, device=dev, dtype=torch.bfloat16, generator=g)
         out = torch.empty(1, n_out, device=dev, dtype=torch.bfloat16)
