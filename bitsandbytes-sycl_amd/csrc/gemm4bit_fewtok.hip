@@ -511,6 +511,16 @@ bool launch_gemm_4bit_fewtok(int m, int n, int k, const T* A, int lda, const uin
   if (g_fewtok_mode >= 16) return false;                    // (the ablation kernels exist in the lab build only)
 #else
   if (g_fewtok_mode >= 16) {                                // lab ablations: nested, <= 8 tokens, 48-row workgroups
+    if (nested && s4 && rg == 3 && n > 16 && n <= 32) {     // (round 6: 17..32 tokens, timeline + ablations)
+      switch (g_fewtok_mode - 16) {
+        case 128: go(k_gemm_4bit_fewtok<T, 3, 2, true, true, 8, false, 128>, 8); return true;
+        case 129: go(k_gemm_4bit_fewtok<T, 3, 2, true, true, 8, false, 129>, 8); return true;
+        case 130: go(k_gemm_4bit_fewtok<T, 3, 2, true, true, 8, false, 130>, 8); return true;
+        case 132: go(k_gemm_4bit_fewtok<T, 3, 2, true, true, 8, false, 132>, 8); return true;
+        case 135: go(k_gemm_4bit_fewtok<T, 3, 2, true, true, 8, false, 135>, 8); return true;
+        default: return false;
+      }
+    }
     if (!nested || n > 8 || !s4) return false;
     constexpr bool X8L = true;
     if (rg == 1) {                                          // (timeline of the 16-row form)
