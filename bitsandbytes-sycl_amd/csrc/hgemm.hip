@@ -135,6 +135,34 @@ __device__ __forceinline__ void glds16_chain(const void* sbase, uint32_t voff) {
 }
 __device__ __forceinline__ void hg_set_m0(uint32_t lds) { asm volatile("s_mov_b32 m0, %0" : : "s"(lds) : "memory"); }
 
+// HG_DMA_BUF (round-6 A/B build switch): the LDS-DMA pieces as MUBUF `buffer_load_dwordx4 ... offen lds` (a buffer
+// resource over the operand, the k-tile's byte offset in soffset, the same per-piece VGPR offsets) instead of the
+// FLAT-encoded `global_load_lds_dwordx4`.  Same bytes to the same LDS slots, bit-identical outputs -- and 2.5-3.4 %
+// slower (metric shape 230.0 -> 237.1 us, 4096^3 90.4 -> 93.5, int8 121.9 -> 124.9; tools/r06_hg_variant.sh,
+// profiles/lab/r06_hg_dma_buf_ab.json), so the library keeps the FLAT form (0).
+#ifndef HG_DMA_BUF
+#define HG_DMA_BUF 0
+#endif
+typedef int hg_rsrc_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ hg_rsrc_t hg_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  // dword1: base[47:32], stride 0; dword2: num_records (no range check in practice: the offsets stay < 4 GiB);
+  // dword3: the raw-buffer word of common.hpp's loads (DATA_FORMAT 32)
+  hg_rsrc_t r = {(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xFFFFu), -1, 0x00020000};
+  r[0] = __builtin_amdgcn_readfirstlane(r[0]);
+  r[1] = __builtin_amdgcn_readfirstlane(r[1]);
+  return r;
+}
+template <int STEP>
+__device__ __forceinline__ void glds16_chain_buf(hg_rsrc_t rsrc, uint32_t voff, uint32_t soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_add_u32 m0, m0, %3" : : "v"(voff), "s"(rsrc), "s"(soff), "i"(STEP)
+               : "memory");
+}
+__device__ __forceinline__ void glds16_buf_m0(hg_rsrc_t rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+               : "memory");
+}
+
 __device__ __forceinline__ int hg_swz(int r, int s) { return r * 128 + ((s ^ ((r >> 1) & 7)) << 4); }
 
 // one dword per lane by LDS-DMA (lane l -> lds + 4 l), scalar base + 32-bit lane offset, M0 written here
@@ -590,12 +618,15 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
   }
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem);
   const uint32_t ldsA0 = lds_base + wave * WI * 1024, ldsB0 = lds_base + TA + wave * WJ * 1024;
+  [[maybe_unused]] const hg_rsrc_t rsA = hg_rsrc(A), rsB = hg_rsrc(B);
   auto dma_a = [&](int kt, int st, int i) {
-    if constexpr ((V & 16) != 0) glds16_sv_m0(A + (long long)kt * 128, aoff[i], ldsA0 + st * STG + i * 1024);
+    if constexpr (HG_DMA_BUF && (V & 16) != 0) glds16_buf_m0(rsA, aoff[i], (uint32_t)kt * 128u, ldsA0 + st * STG + i * 1024);
+    else if constexpr ((V & 16) != 0) glds16_sv_m0(A + (long long)kt * 128, aoff[i], ldsA0 + st * STG + i * 1024);
     else glds16_sv(A + (long long)kt * 128, aoff[i], ldsA0 + st * STG + i * 1024);
   };
   auto dma_b = [&](int kt, int st, int i) {
-    if constexpr ((V & 16) != 0) glds16_sv_m0(B + (long long)kt * 128, boff[i], ldsB0 + st * STG + i * 1024);
+    if constexpr (HG_DMA_BUF && (V & 16) != 0) glds16_buf_m0(rsB, boff[i], (uint32_t)kt * 128u, ldsB0 + st * STG + i * 1024);
+    else if constexpr ((V & 16) != 0) glds16_sv_m0(B + (long long)kt * 128, boff[i], ldsB0 + st * STG + i * 1024);
     else glds16_sv(B + (long long)kt * 128, boff[i], ldsB0 + st * STG + i * 1024);
   };
 
@@ -810,9 +841,15 @@ k_hgemm(int M, int N, int K, const void* __restrict__ Av, long long lda, const v
       }
       if constexpr (!L) {
         if constexpr (q == P3::SETB) hg_set_m0(ldsB0 + st * STG);
-        if constexpr (P3::bpiece(q) >= 0 && (HG_P3_ABL & 16) == 0) glds16_chain<1024>(B + (long long)kn * 128, boff[P3::bpiece(q)]);
+        if constexpr (P3::bpiece(q) >= 0 && (HG_P3_ABL & 16) == 0) {
+          if constexpr (HG_DMA_BUF) glds16_chain_buf<1024>(rsB, boff[P3::bpiece(q)], (uint32_t)kn * 128u);
+          else glds16_chain<1024>(B + (long long)kn * 128, boff[P3::bpiece(q)]);
+        }
         if constexpr (q == P3::SETA) hg_set_m0(ldsA0 + st * STG);
-        if constexpr (P3::apiece(q) >= 0 && (HG_P3_ABL & 16) == 0) glds16_chain<1024>(A + (long long)kn * 128, aoff[P3::apiece(q)]);
+        if constexpr (P3::apiece(q) >= 0 && (HG_P3_ABL & 16) == 0) {
+          if constexpr (HG_DMA_BUF) glds16_chain_buf<1024>(rsA, aoff[P3::apiece(q)], (uint32_t)kn * 128u);
+          else glds16_chain<1024>(A + (long long)kn * 128, aoff[P3::apiece(q)]);
+        }
         if constexpr (q == P3::B3) {
           // (HG_P3_ABL lab bits: 4 = no vmcnt wait at B3, 8 = no barrier at B3 -- timing only)
           if constexpr ((HG_P3_ABL & 4) == 0) {
